@@ -1,0 +1,138 @@
+"""Writes the benchmark scenes in the reference's JSON schema.
+
+The scenes are re-authored (not copied): the Cornell box is the standard
+public 555-unit box (walls, ceiling light, two blocks) as the reference
+configures it in scenes/cornell_box.json, plus its ray-marched Heart
+(BruteForsableShape); spheres.json is the reference's ground + glass + heart
+arrangement.  The schema is SceneJson (src/world/json_models.rs:23-29).
+
+    python scenes/make_scenes.py            # writes cornell_box.json, spheres.json
+    python scenes/make_scenes.py --synthetic N   # also synthetic_N.json (config C5)
+"""
+import argparse
+import json
+import random
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+
+
+def tr(t, r=(0, 0, 0), s=(1, 1, 1)):
+    return {"translate": list(t), "rotate": list(r), "scale": list(s)}
+
+
+def solid(c):
+    return {"type": "SolidColor", "color": list(c)}
+
+
+def lambert(c):
+    return {"type": "Lambertian", "albedo": solid(c)}
+
+
+def cornell():
+    def wall(t, r, mat, x=(0, 555), y=(0, 555)):
+        return {"type": "Rectangle", "x0": x[0], "x1": x[1], "y0": y[0], "y1": y[1],
+                "transform": tr(t, r), "material": mat}
+
+    shapes = [
+        wall((555, 0, 555), (0, 90, 0), "Green"),
+        wall((0, 0, 555), (0, 90, 0), "Red"),
+        wall((0, 0, 0), (90, 0, 0), "White"),
+        wall((0, 555, 0), (90, 0, 0), "White"),
+        wall((555, 0, 555), (0, 0, 90), "White"),
+        wall((0, 554, 0), (90, 0, 0), "Light", x=(213, 343), y=(227, 332)),
+        {"type": "Cube", "name": "Cube1", "transform": tr((347.5, 165, 377.5), (0, 15, 0), (82.5, 165, 82.5)),
+         "material": "White"},
+        {"type": "Cube", "name": "Cube2", "transform": tr((212.5, 82.5, 147.5), (0, -18, 0), (82.5, 82.5, 82.5)),
+         "material": "White"},
+        {"type": "BruteForsableShape", "name": "Heart", "shape": {"type": "Heart", "sphere_radius": 1.45},
+         "step": 0.01, "transform": tr((212.5, 200, 147.5), (-95, -18, 0), (82.5, 82.5, 82.5)),
+         "material": "Red"},
+    ]
+    return {
+        "camera": {"position": [278, 278, -800], "direction": [0, 0, 1], "up": [0, 1, 0],
+                   "fov": 40, "focal_length": 1},
+        "shapes": shapes,
+        "materials": {
+            "Green": lambert((0.12, 0.45, 0.15)),
+            "Red": lambert((0.65, 0.05, 0.05)),
+            "White": lambert((0.73, 0.73, 0.73)),
+            "Light": {"type": "DiffuseLight", "emit": solid((15, 15, 15))},
+        },
+        "background": [0, 0, 0],
+    }
+
+
+def spheres():
+    shapes = [
+        {"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+         "material": "Ground"},
+        {"type": "Sphere", "name": "GlassSphere", "transform": tr((0, 1, 0), (-90, 0, 0)), "material": "Glass"},
+        {"type": "Sphere", "name": "GlassSphereInside", "transform": tr((0, 1, 0), s=(0.5, 0.5, 0.5)),
+         "material": "Glass", "inverse_normal": True},
+        {"type": "BruteForsableShape", "name": "Heart2", "shape": {"type": "Heart"}, "step": 0.01,
+         "transform": tr((-4, 1, 0), (-90, 25, 0)), "material": "Brown"},
+        {"type": "BruteForsableShape", "name": "Heart3", "shape": {"type": "Heart"}, "step": 0.01,
+         "transform": tr((4, 2, 0), (-90, -25, 0)), "material": "Mirror"},
+    ]
+    return {
+        "camera": {"position": [-0.6, 7, -69], "direction": [0.6, -7, 69], "up": [0, 1, 0],
+                   "fov": 20, "focal_length": 1},
+        "shapes": shapes,
+        "materials": {
+            "Ground": lambert((0.5, 0.5, 0.5)),
+            "Glass": {"type": "Dielectric", "index_of_refraction": 1.5},
+            "Brown": lambert((0.4, 0.2, 0.1)),
+            "Mirror": {"type": "Metal", "albedo": solid((0.7, 0.6, 0.5)), "fuzz": 0},
+        },
+        "background": [0, 0, 0],
+    }
+
+
+def synthetic(n, seed=1):
+    """C5: n small spheres on a jittered grid (add_random_spheres recipe scaled up,
+    json_models.rs:73-133), a Lambertian ground sphere and the spheres.json camera."""
+    rng = random.Random(seed)
+    side = int(round(n ** 0.5))
+    mats = {"Ground": lambert((0.5, 0.5, 0.5))}
+    shapes = [{"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+               "material": "Ground"}]
+    half = side // 2
+    k = 0
+    for a in range(-half, side - half):
+        for b in range(-half, side - half):
+            if k >= n:
+                break
+            c = (a * 0.5 + 0.45 * rng.random(), 0.2, b * 0.5 + 0.45 * rng.random())
+            roll = rng.random()
+            name = "M%d" % k
+            if roll < 0.8:
+                col = [rng.random() ** 2 for _ in range(3)]
+                mats[name] = lambert(col)
+            elif roll < 0.95:
+                mats[name] = {"type": "Metal", "albedo": solid([0.5 * (1 - rng.random()) for _ in range(3)]),
+                              "fuzz": 0.5 * rng.random()}
+            else:
+                mats[name] = {"type": "Dielectric", "index_of_refraction": 1.5}
+            shapes.append({"type": "Sphere", "name": "S%d" % k, "transform": tr(c, s=(0.2, 0.2, 0.2)),
+                           "material": name})
+            k += 1
+    return {
+        "camera": {"position": [13, 2, 3], "direction": [-13, -2, -3], "up": [0, 1, 0], "fov": 20,
+                   "focal_length": 1},
+        "shapes": shapes, "materials": mats, "background": [0, 0, 0],
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--synthetic", type=int, default=0)
+    a = ap.parse_args()
+    (HERE / "cornell_box.json").write_text(json.dumps(cornell(), indent=1) + "\n")
+    (HERE / "spheres.json").write_text(json.dumps(spheres(), indent=1) + "\n")
+    if a.synthetic:
+        (HERE / ("synthetic_%d.json" % a.synthetic)).write_text(json.dumps(synthetic(a.synthetic)) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,227 @@
+"""Benchmark: Msamples/s on cornell_box 1920x1080, 256 spp, 8 bounces (BASELINE.json configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one full frame (all W*H*spp camera samples, every bounce) rendered
+from scene data resident in HBM into an HBM frame buffer.  For N > 1 the
+frame's 16x16 tiles are dealt round-robin to the ranks (tile k -> rank k % N),
+each rank renders its tiles into a compact shard, the shards are gathered to
+rank 0 over RCCL (torch.distributed "nccl") and un-interleaved there: the same
+frame at every N ("scaling": "strong").  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Msamples/sec cornell_box 1920x1080x256spp at 1/2/4/8 MI355X; RMS pixel delta"
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (FMA = 2 FLOP); no-FMA instruction peak is half of it
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
+
+# FLOPs per event of the kernel's traversal policy (counted from pt_device.hpp;
+# f64 add/sub/mul/div/sqrt = 1 each, compares and min/max not counted).
+FLOP_WEIGHTS = {
+    "camera": 28,          # jittered ray + normalize
+    "leaf_xform": 33,      # inverse transform of the ray (point 18 + vector 15)
+    "sphere": 19, "rect": 4, "cube": 12, "march_bound": 31,
+    "march_step": 19,      # t += step, p += c (4) + heart_f (15)
+    "bounce": 100,         # finish(): object hit point/normal, normalisations, world transforms
+    "lambert": 20, "reject_try": 14, "metal": 25, "dielectric": 40,
+}
+
+
+def flops_per_sample(st):
+    w = FLOP_WEIGHTS
+    tests = sum(st["shape_tests"])
+    f = (w["camera"] * st["samples"] + w["leaf_xform"] * tests + w["sphere"] * st["shape_tests"][0]
+         + w["rect"] * st["shape_tests"][1] + w["cube"] * st["shape_tests"][2]
+         + w["march_bound"] * st["march_bounds"] + w["march_step"] * st["march_steps"]
+         + w["bounce"] * st["bounces"] + w["lambert"] * st["scatters"][0] + w["reject_try"] * st["rejection_tries"]
+         + w["metal"] * st["scatters"][1] + w["dielectric"] * st["scatters"][2])
+    return f / max(1, st["samples"])
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="cornell_box.json")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--scene-seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--parity-pixels", type=int, default=48)
+    return ap.parse_args()
+
+
+def cpu_baseline(text, args, threads):
+    """Oracle in the reference's BvhNode mode (the reference threaded renderer's
+    algorithm) on a bounded sample: every k-th row of the frame at 1 spp."""
+    import numpy as np
+    import oracle
+    sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
+    w, h = args.width, args.height
+    probe_rows = np.arange(0, h, max(1, h // 8))
+    px = (probe_rows[:, None] * w + np.arange(0, w, 8)[None, :]).ravel().astype(np.uint32)
+    t = time.perf_counter()
+    sc.render(w, h, 1, args.depth, args.seed, pixels=px, threads=threads)
+    rate = len(px) / max(1e-9, time.perf_counter() - t)
+    nrows = int(min(h, max(1, args.cpu_seconds * rate / w)))
+    stride = max(1, h // nrows)
+    rows = np.arange(stride // 2, h, stride)[:nrows]
+    px = (rows[:, None] * w + np.arange(w)[None, :]).ravel().astype(np.uint32)
+    t = time.perf_counter()
+    sc.render(w, h, 1, args.depth, args.seed, pixels=px, threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": round(len(px) / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "%d full rows (every %dth) of the %dx%d frame at 1 spp, depth %d = %d samples in %.1f s; "
+                      "oracle with the reference's BvhNode traversal, step_by_step chunking"
+                      % (len(rows), stride, w, h, args.depth, len(px), dt)}
+
+
+def algorithmic_flops(text, args):
+    """F (FLOP/sample) of the GPU kernel's policy (linear closest-hit scan, exact
+    fixed-step march), from oracle event counts on a strided pixel sample."""
+    import numpy as np
+    import oracle
+    sc = oracle.Scene(text, seed=args.scene_seed)
+    w, h = args.width, args.height
+    px = (np.arange(3, h, 24)[:, None] * w + np.arange(5, w, 24)[None, :]).ravel().astype(np.uint32)
+    _, st = sc.render(w, h, 2, args.depth, args.seed, pixels=px, stats=True)
+    return flops_per_sample(st), st
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import __graft_entry__ as ge
+    pt = ge.load_package()
+    text = (ROOT / "scenes" / args.scene).read_text()
+    scene = pt.Scene.from_json(text, seed=args.scene_seed)
+    r = pt.HipRenderer(scene, device=local, depth=args.depth)
+    cam = scene.camera()
+    W, H, spp = args.width, args.height, args.spp
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
+    per = pt.shard_tiles(W, H, 0, world)
+    if world > 1:
+        shard = torch.zeros(per * 256 * 3, dtype=torch.float64, device="cuda")
+        gathered = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda") if rank == 0 else None
+        glist = list(gathered.view(world, -1).unbind(0)) if rank == 0 else None
+    torch.cuda.synchronize()
+
+    k_start, k_end = [], []
+
+    def step():
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        if world == 1:
+            r.render_device(cam, W, H, spp, args.seed, 0, 1, frame.data_ptr(), sp)
+        else:
+            r.render_device(cam, W, H, spp, args.seed, rank, world, shard.data_ptr(), sp)
+        ev1.record(stream)
+        k_start.append(ev0)
+        k_end.append(ev1)
+        if world > 1:
+            dist.gather(shard, glist, dst=0)
+            if rank == 0:
+                pt.unshard_device(gathered.data_ptr(), W, H, world, frame.data_ptr(), sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    k_start.clear()
+    k_end.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms_max = t.tolist()
+    else:
+        kernel_ms_max = kernel_ms
+
+    if rank == 0:
+        samples_frame = W * H * spp
+        value = samples_frame * args.steps / elapsed / 1e6
+        img = frame.view(-1, 3).cpu().numpy()
+        sys.path.insert(0, str(ROOT / "oracle"))
+        threads = min(16, os.cpu_count() or 1)
+
+        # roofline of the dominant kernel (render_tiles), this rank's launches
+        F, _ = algorithmic_flops(text, args)
+        my_tiles = pt.shard_tiles(W, H, rank, world)
+        samples_launch = samples_frame * my_tiles / (pt.shard_tiles(W, H, 0, 1))
+        achieved = F * samples_launch / (kernel_ms / 1e3) / 1e12
+        out_bytes = 24.0 * W * H * my_tiles / pt.shard_tiles(W, H, 0, 1)
+        rec = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: re-authored cornell_box.json, add_random_spheres from seed %d" % args.scene_seed,
+            "config": {"workload": "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth),
+                       "width": W, "height": H, "spp": spp, "depth": args.depth, "seed": args.seed,
+                       "parallelism": "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"},
+            "roofline": {"bound": "valu_f64", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
+                         "flops_per_sample": round(F, 1), "kernel": "render_tiles",
+                         "kernel_ms_avg": round(kernel_ms, 3), "kernel_ms_max_rank": round(kernel_ms_max, 3)},
+            "roofline_hbm": {"achieved": round(out_bytes / (kernel_ms / 1e3) / 1e9, 4), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                             "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
+        }
+        if not args.no_parity:
+            import oracle
+            rng = np.random.default_rng(1234)
+            px = rng.choice(W * H, size=args.parity_pixels, replace=False).astype(np.uint32)
+            sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
+            ref = sc.render(W, H, spp, args.depth, args.seed, pixels=px, threads=threads)
+            got = img[px]
+            rec["rms_vs_oracle"] = float(np.sqrt(np.mean((got - ref) ** 2)))
+            rec["rms_pixels"] = int(len(px))
+            rec["exact_pixels_frac"] = float(np.mean(np.all(got == ref, axis=1)))
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(text, args, threads)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * rs_pathtracing.h — C-ABI boundary of the MI355X-native path-tracing sample loop.
+ *
+ * This is what the reference's Rust host would bind with `extern "C"` to
+ * replace its CPU renderer (INTEGRATION.md shows the binding).  Each entry
+ * point names the reference interface it replaces (paths relative to the
+ * dkarpushkin/rs-pathtracing checkout).  Plain pointers and sizes only; no
+ * exception or abort crosses this boundary: every call returns a status
+ * (PT_OK = 0, negative = error) and pt_last_error() gives the message of the
+ * last failing call on the calling thread.
+ *
+ * Buffers: colour buffers are `Vec<Vector3d>` laid out as w*h*3 doubles,
+ * row-major, index x + y*w, y = 0 at the top (src/camera/ray_caster.rs:35),
+ * linear radiance (no gamma, no clamp) — the buffer render_step fills in
+ * src/renderer/step_by_step.rs:115-117.
+ */
+#ifndef RS_PATHTRACING_H
+#define RS_PATHTRACING_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_ERR_INVALID -1     /* bad argument / unknown material name           */
+#define PT_ERR_PARSE -2       /* JSON syntax or schema (serde_json::Error)        */
+#define PT_ERR_UNSUPPORTED -3 /* valid reference JSON the GPU path does not take  */
+#define PT_ERR_HIP -4         /* HIP runtime failure                               */
+#define PT_ERR_STATE -5       /* call out of order (e.g. step before start)       */
+
+/* shape kinds */
+#define PT_SPHERE 0    /* src/world/shapes/mod.rs:304-399 */
+#define PT_RECTANGLE 1 /* src/world/shapes/mod.rs:150-221 */
+#define PT_CUBE 2      /* src/world/shapes/mod.rs:223-302 */
+#define PT_MARCH 3     /* RayMarchingShape, src/world/shapes/ray_marching.rs:10-110 */
+#define PT_FUNC_HEART 0
+
+/* material kinds (src/world/material.rs) */
+#define PT_LAMBERTIAN 0
+#define PT_METAL 1
+#define PT_DIELECTRIC 2
+#define PT_DIFFUSE_LIGHT 3
+#define PT_EMPTY 4
+
+typedef struct pt_scene pt_scene;
+typedef struct pt_renderer pt_renderer;
+
+/* Scene::from_json options.  The reference appends ~480 spheres drawn from an
+ * unseeded thread_rng (src/world/json_models.rs:44, 50-133); here the draw is
+ * seeded so a scene is reproducible, and it can be switched off. */
+typedef struct {
+    uint32_t random_spheres; /* 1 = reference behaviour (default), 0 = JSON shapes only */
+    uint32_t reserved;
+    uint64_t seed; /* seed of the add_random_spheres stream */
+} pt_scene_opts;
+
+/* Camera (src/camera/mod.rs:36-46).  fov in radians, as Camera::new takes it. */
+typedef struct {
+    double position[3], direction[3], up[3], right[3];
+    double fov, focal_length;
+} pt_camera;
+
+/* Realized shape record (introspection / parity).  Matrices are 4x4 row-major. */
+typedef struct {
+    int32_t type, material, inverse_normal, depth, func, pad0;
+    double direct[16], inverse[16];
+    double x0, y0, x1, y1, step;
+} pt_shape_info;
+
+typedef struct {
+    int32_t type, pad0;
+    double albedo[3];
+    double fuzz, ior;
+    double emit[3];
+} pt_material_info;
+
+/* RayHit (src/world/ray.rs:21-29) for the closest_hit probe. */
+typedef struct {
+    double t;
+    double point[3];
+    double normal[3];
+    int32_t front_face, shape, material, pad0;
+} pt_hit;
+
+/* ---- scene: Scene::from_json (src/world/mod.rs:46-49) ------------------ */
+int pt_scene_create_from_json(const char *json, size_t len, const pt_scene_opts *opts, pt_scene **out);
+void pt_scene_destroy(pt_scene *scene);
+/* Scene::camera (src/world/mod.rs:193-197) */
+int pt_scene_camera(const pt_scene *scene, pt_camera *out);
+int pt_scene_num_shapes(const pt_scene *scene);
+int pt_scene_get_shape(const pt_scene *scene, int index, pt_shape_info *out);
+int pt_scene_num_materials(const pt_scene *scene);
+int pt_scene_get_material(const pt_scene *scene, int index, pt_material_info *out);
+
+/* Camera::new (src/camera/mod.rs:71-88) */
+int pt_camera_new(const double position[3], const double direction[3], const double up[3],
+                  double focal_length, double fov_radians, pt_camera *out);
+
+/* ---- renderer: trait Renderer (src/renderer/mod.rs:47-56) -------------- */
+/* ThreadPoolRenderer::new(scene, thread_number, depth)
+ * (src/renderer/step_by_step.rs:37): `device` (HIP ordinal, -1 = current)
+ * replaces thread_number.  The scene must outlive the renderer. */
+int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer **out);
+void pt_renderer_destroy(pt_renderer *r);
+/* Renderer::start_rendering (mod.rs:48-53): queues the whole frame on the
+ * GPU and returns at once.  seed keys the per-(pixel, sample) RNG stream. */
+int pt_render_start(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                    uint32_t samples_number, uint64_t seed);
+/* Renderer::render_step (mod.rs:54): copies every finished band of rows into
+ * rgb (w*h*3 doubles) and returns 1 once the frame is complete, 0 while work
+ * is pending (blocking = 0, step_by_step.rs:101-121 semantics), or blocks
+ * until done (blocking = 1, thread_pool_new.rs:96-126 semantics). */
+int pt_render_step(pt_renderer *r, double *rgb, int blocking);
+/* Renderer::stop_rendering (mod.rs:55) */
+int pt_render_stop(pt_renderer *r);
+
+/* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */
+/* Renders this rank's share of the frame straight into device memory on
+ * `hip_stream` (0 = the renderer's stream).  Pixels are cut into 16x16 tiles
+ * numbered row-major; tile k belongs to rank k % world.  world == 1: d_out is
+ * the w*h*3 frame.  world > 1: d_out holds this rank's tiles in order,
+ * pt_shard_tiles(...) * 256 * 3 doubles (pixels outside the frame are 0). */
+int pt_render_device(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                     uint32_t samples_number, uint64_t seed, uint32_t rank, uint32_t world,
+                     double *d_out, void *hip_stream);
+uint32_t pt_shard_tiles(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
+/* Rebuild the frame from `world` gathered shard buffers laid out back to back,
+ * each padded to pt_shard_tiles(w, h, 0, world) tiles. */
+int pt_unshard_device(const double *d_gathered, uint32_t width, uint32_t height, uint32_t world,
+                      double *d_frame, void *hip_stream);
+
+/* ---- probes on the GPU (reference pub fns) ----------------------------- */
+/* Scene::closest_hit (src/world/mod.rs:42-44) for n rays (origin, direction:
+ * 6 doubles each).  out[i].shape = -1 on a miss. */
+int pt_closest_hit(pt_renderer *r, const double *rays, size_t n, double min_t, double max_t,
+                   pt_hit *out);
+/* ray_color (src/renderer/mod.rs:23-45) for n rays; rng_states[i] is the
+ * stream state for ray i and is advanced in place. */
+int pt_ray_color(pt_renderer *r, const double *rays, uint64_t *rng_states, size_t n, uint32_t depth,
+                 double *out);
+/* trace_pixel_samples (src/renderer/mod.rs:151-155) for an explicit list of
+ * pixel indices (x + y*w); out is n*3 means. */
+int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                           uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
+                           double *out);
+
+/* Display encode (src/bin/main.rs:281-289): sqrt -> clamp [0, 0.999] -> *256
+ * -> u8, alpha 255; rgba is w*h*4 bytes. Host-side. */
+int pt_encode_rgba8(const double *rgb, size_t npix, uint8_t *rgba);
+
+/* ---- RNG spec shared with the parity oracle ---------------------------- */
+uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);
+
+const char *pt_last_error(void);
+const char *pt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

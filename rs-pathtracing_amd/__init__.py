@@ -1,0 +1,335 @@
+"""rs_pathtracing_amd — MI355X-native sample loop behind the reference's interfaces.
+
+Python mirror of the reference's host API over the C-ABI in
+include/rs_pathtracing.h (librs_pathtracing_amd.so, built in-tree):
+
+    Scene.from_json(data)                       src/world/mod.rs:46-49
+    Scene.camera()                              src/world/mod.rs:193-197
+    Camera.new(position, direction, up, focal_length, fov)   src/camera/mod.rs:71-88
+    ImageParams(width, height)                  src/camera/ray_caster.rs:10-14
+    Renderer: start_rendering / render_step / stop_rendering   src/renderer/mod.rs:47-56
+    HipRenderer(scene, device, depth)           ThreadPoolRenderer::new, step_by_step.rs:37
+    ray_color / trace_pixel_samples             src/renderer/mod.rs:23-45, 151-155
+    closest_hit                                 src/world/mod.rs:42-44
+
+The colour buffer is the reference's Vec<Vector3d>: a (w*h, 3) float64 array,
+row-major, index x + y*w.  There is no CPU fallback: if the library or a GPU
+is missing, construction fails loudly.
+"""
+from __future__ import annotations
+
+import abc
+import ctypes as C
+import os
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "librs_pathtracing_amd.so"
+
+PT_OK = 0
+PT_ERR_INVALID, PT_ERR_PARSE, PT_ERR_UNSUPPORTED, PT_ERR_HIP, PT_ERR_STATE = -1, -2, -3, -4, -5
+SPHERE, RECTANGLE, CUBE, MARCH = 0, 1, 2, 3
+LAMBERTIAN, METAL, DIELECTRIC, DIFFUSE_LIGHT, EMPTY = 0, 1, 2, 3, 4
+TILE = 16
+
+# every symbol include/rs_pathtracing.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "pt_scene_create_from_json", "pt_scene_destroy", "pt_scene_camera", "pt_scene_num_shapes",
+    "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
+    "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
+    "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
+    "pt_trace_pixel_samples", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+]
+
+
+class PtError(RuntimeError):
+    """A non-zero status from the C-ABI (the reference panics or returns serde_json::Error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__("%s (status %d)" % (msg, code))
+        self.code = code
+
+
+class SceneOpts(C.Structure):
+    _fields_ = [("random_spheres", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_uint64)]
+
+
+class CameraStruct(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("direction", C.c_double * 3), ("up", C.c_double * 3),
+                ("right", C.c_double * 3), ("fov", C.c_double), ("focal_length", C.c_double)]
+
+
+class ShapeInfo(C.Structure):
+    _fields_ = [("type", C.c_int32), ("material", C.c_int32), ("inverse_normal", C.c_int32),
+                ("depth", C.c_int32), ("func", C.c_int32), ("pad0", C.c_int32),
+                ("direct", C.c_double * 16), ("inverse", C.c_double * 16),
+                ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
+                ("step", C.c_double)]
+
+
+class MaterialInfo(C.Structure):
+    _fields_ = [("type", C.c_int32), ("pad0", C.c_int32), ("albedo", C.c_double * 3),
+                ("fuzz", C.c_double), ("ior", C.c_double), ("emit", C.c_double * 3)]
+
+
+class HitStruct(C.Structure):
+    _fields_ = [("t", C.c_double), ("point", C.c_double * 3), ("normal", C.c_double * 3),
+                ("front_face", C.c_int32), ("shape", C.c_int32), ("material", C.c_int32),
+                ("pad0", C.c_int32)]
+
+
+HIT_DTYPE = np.dtype([("t", "<f8"), ("point", "<f8", 3), ("normal", "<f8", 3), ("front_face", "<i4"),
+                      ("shape", "<i4"), ("material", "<i4"), ("pad0", "<i4")])
+assert HIT_DTYPE.itemsize == C.sizeof(HitStruct)
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree HIP library; fails loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError("%s is missing: build it with `make -C rs-pathtracing_amd` or "
+                          "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)"
+                          % LIB_PATH)
+    L = C.CDLL(str(LIB_PATH))
+    vp, d = C.c_void_p, C.POINTER(C.c_double)
+    u32, u64, sz = C.c_uint32, C.c_uint64, C.c_size_t
+    sig = {
+        "pt_scene_create_from_json": (C.c_int, [C.c_char_p, sz, C.POINTER(SceneOpts), C.POINTER(vp)]),
+        "pt_scene_destroy": (None, [vp]),
+        "pt_scene_camera": (C.c_int, [vp, C.POINTER(CameraStruct)]),
+        "pt_scene_num_shapes": (C.c_int, [vp]),
+        "pt_scene_get_shape": (C.c_int, [vp, C.c_int, C.POINTER(ShapeInfo)]),
+        "pt_scene_num_materials": (C.c_int, [vp]),
+        "pt_scene_get_material": (C.c_int, [vp, C.c_int, C.POINTER(MaterialInfo)]),
+        "pt_camera_new": (C.c_int, [d, d, d, C.c_double, C.c_double, C.POINTER(CameraStruct)]),
+        "pt_renderer_create": (C.c_int, [vp, C.c_int, u32, C.POINTER(vp)]),
+        "pt_renderer_destroy": (None, [vp]),
+        "pt_render_start": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64]),
+        "pt_render_step": (C.c_int, [vp, d, C.c_int]),
+        "pt_render_stop": (C.c_int, [vp]),
+        "pt_render_device": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, u32, u32, vp, vp]),
+        "pt_shard_tiles": (u32, [u32, u32, u32, u32]),
+        "pt_unshard_device": (C.c_int, [vp, u32, u32, u32, vp, vp]),
+        "pt_closest_hit": (C.c_int, [vp, d, sz, C.c_double, C.c_double, vp]),
+        "pt_ray_color": (C.c_int, [vp, d, C.POINTER(u64), sz, u32, d]),
+        "pt_trace_pixel_samples": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64,
+                                             C.POINTER(u32), sz, d]),
+        "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
+        "pt_sample_key": (u64, [u64, u64, u64]),
+        "pt_last_error": (C.c_char_p, []),
+        "pt_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(status: int) -> int:
+    if status < 0:
+        raise PtError(status, lib().pt_last_error().decode("utf-8", "replace"))
+    return status
+
+
+def _d3(v):
+    return (C.c_double * 3)(*[float(x) for x in v])
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+@dataclass
+class ImageParams:
+    """src/camera/ray_caster.rs:10-14"""
+    width: int
+    height: int
+
+
+class Camera:
+    """Camera (src/camera/mod.rs:36-46); fov in radians as Camera::new takes it."""
+
+    def __init__(self, c: CameraStruct):
+        self._c = c
+
+    @classmethod
+    def new(cls, position, direction, up, focal_length: float, fov: float) -> "Camera":
+        c = CameraStruct()
+        _check(lib().pt_camera_new(_d3(position), _d3(direction), _d3(up), float(focal_length), float(fov),
+                                   C.byref(c)))
+        return cls(c)
+
+    position = property(lambda s: np.array(s._c.position[:]))
+    direction = property(lambda s: np.array(s._c.direction[:]))
+    up = property(lambda s: np.array(s._c.up[:]))
+    right = property(lambda s: np.array(s._c.right[:]))
+    fov = property(lambda s: s._c.fov)
+    focal_length = property(lambda s: s._c.focal_length)
+
+
+class Scene:
+    """Realized scene: JSON shapes in file order, then add_random_spheres."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def from_json(cls, data: str | bytes, random_spheres: bool = True, seed: int = 1) -> "Scene":
+        raw = data.encode("utf-8") if isinstance(data, str) else bytes(data)
+        opts = SceneOpts(1 if random_spheres else 0, 0, seed)
+        h = C.c_void_p()
+        _check(lib().pt_scene_create_from_json(raw, len(raw), C.byref(opts), C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.pt_scene_destroy(h)
+            self._h = None
+
+    def camera(self) -> Camera:
+        c = CameraStruct()
+        _check(lib().pt_scene_camera(self._h, C.byref(c)))
+        return Camera(c)
+
+    @property
+    def num_shapes(self) -> int:
+        return _check(lib().pt_scene_num_shapes(self._h))
+
+    @property
+    def num_materials(self) -> int:
+        return _check(lib().pt_scene_num_materials(self._h))
+
+    def shape(self, i: int) -> ShapeInfo:
+        s = ShapeInfo()
+        _check(lib().pt_scene_get_shape(self._h, i, C.byref(s)))
+        return s
+
+    def material(self, i: int) -> MaterialInfo:
+        m = MaterialInfo()
+        _check(lib().pt_scene_get_material(self._h, i, C.byref(m)))
+        return m
+
+
+class Renderer(abc.ABC):
+    """trait Renderer (src/renderer/mod.rs:47-56)."""
+
+    @abc.abstractmethod
+    def start_rendering(self, camera: Camera, img_params: ImageParams, samples_number: int): ...
+
+    @abc.abstractmethod
+    def render_step(self, buffer: np.ndarray) -> bool: ...
+
+    @abc.abstractmethod
+    def stop_rendering(self): ...
+
+
+class HipRenderer(Renderer):
+    """The MI355X renderer: ThreadPoolRenderer::new(scene, thread_number, depth)
+    with a HIP device in place of the thread pool.  `seed` keys the per-(pixel,
+    sample) RNG; render_step(blocking=False) is step_by_step's non-blocking
+    drain, blocking=True is thread_pool_new's."""
+
+    def __init__(self, scene: Scene, device: int = -1, depth: int = 50, seed: int = 1):
+        self.scene = scene  # must outlive the renderer
+        self.depth = int(depth)
+        self.seed = int(seed)
+        h = C.c_void_p()
+        _check(lib().pt_renderer_create(scene._h, int(device), self.depth, C.byref(h)))
+        self._h = h
+        self._shape = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.pt_renderer_destroy(h)
+            self._h = None
+
+    def start_rendering(self, camera: Camera, img_params: ImageParams, samples_number: int, seed=None):
+        s = self.seed if seed is None else int(seed)
+        _check(lib().pt_render_start(self._h, C.byref(camera._c), img_params.width, img_params.height,
+                                     int(samples_number), s))
+        self._shape = (img_params.width * img_params.height, 3)
+
+    def render_step(self, buffer: np.ndarray, blocking: bool = False) -> bool:
+        if self._shape is None:
+            raise PtError(PT_ERR_STATE, "render_step before start_rendering")
+        if buffer.shape != self._shape or buffer.dtype != np.float64 or not buffer.flags.c_contiguous:
+            raise ValueError("buffer must be a C-contiguous float64 array of shape %r" % (self._shape,))
+        return _check(lib().pt_render_step(self._h, _dptr(buffer), 1 if blocking else 0)) == 1
+
+    def stop_rendering(self):
+        _check(lib().pt_render_stop(self._h))
+
+    def render(self, camera: Camera, img_params: ImageParams, samples_number: int, seed=None) -> np.ndarray:
+        buf = np.zeros((img_params.width * img_params.height, 3), dtype=np.float64)
+        self.start_rendering(camera, img_params, samples_number, seed)
+        self.render_step(buf, blocking=True)
+        return buf
+
+    def render_device(self, camera: Camera, width: int, height: int, spp: int, seed: int, rank: int,
+                      world: int, out_ptr: int, stream_ptr: int = 0):
+        """Render this rank's tiles into device memory at out_ptr (see pt_render_device)."""
+        _check(lib().pt_render_device(self._h, C.byref(camera._c), width, height, spp, seed, rank, world,
+                                      C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
+
+    # ---- probes --------------------------------------------------------
+    def closest_hit(self, rays: np.ndarray, min_t: float = 0.001, max_t: float = float("inf")) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        out = np.zeros(len(rays), dtype=HIT_DTYPE)
+        _check(lib().pt_closest_hit(self._h, _dptr(rays), len(rays), min_t, max_t, out.ctypes.data))
+        return out
+
+    def ray_color(self, rays: np.ndarray, rng_states: np.ndarray, depth: int | None = None) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        states = np.ascontiguousarray(rng_states, dtype=np.uint64)
+        out = np.zeros((len(rays), 3), dtype=np.float64)
+        _check(lib().pt_ray_color(self._h, _dptr(rays), states.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                  len(rays), self.depth if depth is None else int(depth), _dptr(out)))
+        rng_states[...] = states
+        return out
+
+    def trace_pixel_samples(self, camera: Camera, img_params: ImageParams, samples_number: int,
+                            pixels: np.ndarray, seed=None) -> np.ndarray:
+        pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
+        out = np.zeros((len(pixels), 3), dtype=np.float64)
+        s = self.seed if seed is None else int(seed)
+        _check(lib().pt_trace_pixel_samples(self._h, C.byref(camera._c), img_params.width, img_params.height,
+                                            int(samples_number), s,
+                                            pixels.ctypes.data_as(C.POINTER(C.c_uint32)), len(pixels),
+                                            _dptr(out)))
+        return out
+
+
+def shard_tiles(width: int, height: int, rank: int, world: int) -> int:
+    return lib().pt_shard_tiles(width, height, rank, world)
+
+
+def unshard_device(gathered_ptr: int, width: int, height: int, world: int, frame_ptr: int, stream_ptr: int = 0):
+    _check(lib().pt_unshard_device(C.c_void_p(gathered_ptr), width, height, world, C.c_void_p(frame_ptr),
+                                   C.c_void_p(stream_ptr)))
+
+
+def encode_rgba8(buffer: np.ndarray) -> np.ndarray:
+    """Display encode of src/bin/main.rs:281-289 (gamma 2, clamp, u8)."""
+    buf = np.ascontiguousarray(buffer, dtype=np.float64).reshape(-1, 3)
+    out = np.zeros((len(buf), 4), dtype=np.uint8)
+    _check(lib().pt_encode_rgba8(_dptr(buf), len(buf), out.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return out
+
+
+def sample_key(seed: int, pixel: int, sample: int) -> int:
+    return lib().pt_sample_key(seed, pixel, sample)
+
+
+def version() -> str:
+    return lib().pt_version().decode()

@@ -1,0 +1,168 @@
+// pt_kernel.hip — MI355X (gfx950) kernels of the sample path.
+//
+// render_tiles: the megakernel.  One workgroup = one 16x16 pixel tile,
+// 4 wave64s of 8x8 pixels each (adjacent pixels share a wave, so primary rays
+// and their first bounces stay coherent); one pixel per lane, its spp camera
+// samples traced in order and summed in f64 in registers; one write of the
+// per-pixel mean.  Tiles are dealt round-robin to ranks (tile k -> k % world)
+// so multi-GPU shards balance the Heart-heavy region.
+#include <hip/hip_runtime.h>
+
+#include "pt_device.hpp"
+#include "pt_kernel.hpp"
+
+namespace pt {
+
+using dev::Ray;
+using dev::V3;
+
+template <int NW>
+__global__ __launch_bounds__(256) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
+    const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
+    const uint32_t k = P.rank + ti * P.world;       // global tile id
+    const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t lx = ((w & 1u) << 3) | (l & 7u), ly = ((w >> 1) << 3) | (l >> 3);
+    const uint32_t x = tx * TILE + lx, y = ty * TILE + ly;
+    double *dst = P.compact ? out + ((size_t)ti * (TILE * TILE) + ly * TILE + lx) * 3
+                            : out + ((size_t)y * P.width + x) * 3;
+    if (x >= P.width || y >= P.height) {
+        if (P.compact) dst[0] = dst[1] = dst[2] = 0.0;
+        return;
+    }
+    V3 c = dev::trace_pixel<NW>(sc, P, x, y);
+    dst[0] = c.x;
+    dst[1] = c.y;
+    dst[2] = c.z;
+}
+
+__global__ void unshard(const double *__restrict__ g, uint32_t width, uint32_t height, uint32_t world,
+                        uint32_t tiles_x, uint32_t per_rank, double *__restrict__ frame) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)width * height) return;
+    uint32_t x = (uint32_t)(i % width), y = (uint32_t)(i / width);
+    uint32_t k = (y / TILE) * tiles_x + x / TILE;
+    uint32_t rank = k % world, ti = k / world;
+    const double *s = g + (((size_t)rank * per_rank + ti) * (TILE * TILE) + (y % TILE) * TILE + x % TILE) * 3;
+    frame[i * 3 + 0] = s[0];
+    frame[i * 3 + 1] = s[1];
+    frame[i * 3 + 2] = s[2];
+}
+
+__global__ void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays, size_t n, double min_t,
+                                  double max_t, pt_hit *__restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r;
+    r.o = dev::v3(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
+    r.d = dev::v3(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
+    double t;
+    int who = dev::closest(sc.shapes, sc.nshapes, r, min_t, max_t, &t);
+    pt_hit h = {};
+    h.shape = who;
+    h.material = -1;
+    if (who >= 0) {
+        dev::Hit hh = dev::finish(sc.shapes[who], r, t);
+        h.t = t;
+        h.point[0] = hh.p.x;
+        h.point[1] = hh.p.y;
+        h.point[2] = hh.p.z;
+        h.normal[0] = hh.n.x;
+        h.normal[1] = hh.n.y;
+        h.normal[2] = hh.n.z;
+        h.front_face = hh.front ? 1 : 0;
+        h.material = sc.shapes[who].material;
+    }
+    out[i] = h;
+}
+
+template <int NW>
+__global__ void ray_color_probe(dev::Scene sc, const double *__restrict__ rays, uint64_t *__restrict__ states,
+                                size_t n, uint32_t depth, double s11, double *__restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ray r;
+    r.o = dev::v3(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
+    r.d = dev::v3(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
+    dev::Rng rng{states[i]};
+    V3 c = dev::ray_color<NW>(sc, r, depth, rng, s11);
+    states[i] = rng.s;
+    out[i * 3 + 0] = c.x;
+    out[i * 3 + 1] = c.y;
+    out[i * 3 + 2] = c.z;
+}
+
+template <int NW>
+__global__ void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
+                                   double *__restrict__ out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t idx = pixels[i];
+    V3 c = dev::trace_pixel<NW>(sc, P, idx % P.width, idx / P.width);
+    out[i * 3 + 0] = c.x;
+    out[i * 3 + 1] = c.y;
+    out[i * 3 + 2] = c.z;
+}
+
+// ------------------------------------------------------------- launchers
+static dev::Scene dscene(const DeviceScene &s) { return dev::Scene{s.shapes, s.mats, s.nshapes}; }
+
+// Attenuation-stack width by depth: one 32-bit material id per bounce.
+#define PT_DISPATCH_NW(depth, CALL)        \
+    do {                                   \
+        if ((depth) <= 8) {                \
+            constexpr int NW = 4;          \
+            CALL;                          \
+        } else if ((depth) <= 16) {        \
+            constexpr int NW = 8;          \
+            CALL;                          \
+        } else if ((depth) <= 32) {        \
+            constexpr int NW = 16;         \
+            CALL;                          \
+        } else {                           \
+            constexpr int NW = 32;         \
+            CALL;                          \
+        }                                  \
+    } while (0)
+
+hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st) {
+    if (P.tile_count == 0) return hipSuccess;
+    PT_DISPATCH_NW(P.depth, (render_tiles<NW><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out)));
+    return hipGetLastError();
+}
+
+hipError_t launch_unshard(const double *g, uint32_t width, uint32_t height, uint32_t world, double *frame,
+                          hipStream_t st) {
+    uint32_t tiles_x = (width + TILE - 1) / TILE, tiles_y = (height + TILE - 1) / TILE;
+    uint32_t total = tiles_x * tiles_y;
+    uint32_t per_rank = (total + world - 1) / world;
+    size_t npix = (size_t)width * height;
+    unsigned blocks = (unsigned)((npix + 255) / 256);
+    if (blocks) unshard<<<blocks, 256, 0, st>>>(g, width, height, world, tiles_x, per_rank, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_closest_hit(const DeviceScene &s, const double *rays, size_t n, double min_t, double max_t,
+                              pt_hit *out, hipStream_t st) {
+    if (!n) return hipSuccess;
+    closest_hit_probe<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dscene(s), rays, n, min_t, max_t, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_ray_color(const DeviceScene &s, const double *rays, uint64_t *states, size_t n, uint32_t depth,
+                            double s11, double *out, hipStream_t st) {
+    if (!n) return hipSuccess;
+    PT_DISPATCH_NW(depth, (ray_color_probe<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+                              dscene(s), rays, states, n, depth, s11, out)));
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
+                               double *out, hipStream_t st) {
+    if (!n) return hipSuccess;
+    PT_DISPATCH_NW(P.depth, (trace_pixels_probe<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+                                dscene(s), P, pixels, n, out)));
+    return hipGetLastError();
+}
+
+}  // namespace pt

@@ -1,0 +1,26 @@
+// pt_kernel.hpp — host-side launchers of the HIP kernels (pt_kernel.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/rs_pathtracing.h"
+#include "pt_types.hpp"
+
+namespace pt {
+
+struct DeviceScene {
+    DShape *shapes = nullptr;
+    DMaterial *mats = nullptr;
+    int nshapes = 0, nmats = 0;
+};
+
+hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st);
+hipError_t launch_unshard(const double *gathered, uint32_t width, uint32_t height, uint32_t world, double *frame,
+                          hipStream_t st);
+hipError_t launch_closest_hit(const DeviceScene &s, const double *rays, size_t n, double min_t, double max_t,
+                              pt_hit *out, hipStream_t st);
+hipError_t launch_ray_color(const DeviceScene &s, const double *rays, uint64_t *states, size_t n, uint32_t depth,
+                            double s11, double *out, hipStream_t st);
+hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
+                               double *out, hipStream_t st);
+
+}  // namespace pt

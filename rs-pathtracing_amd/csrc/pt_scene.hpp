@@ -1,0 +1,58 @@
+// pt_scene.hpp — host-side scene realization: Scene::from_json
+// (src/world/mod.rs:46-49 -> json_models.rs:31-48), InversableTransform
+// (src/algebra/transform.rs:16-23), Camera::new (src/camera/mod.rs:71-88) and
+// the ray-caster constants (src/camera/ray_caster.rs:30-48).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rs_pathtracing.h"
+#include "pt_types.hpp"
+
+namespace pt {
+
+struct HostShape {
+    int32_t type = 0, material = 0, inverse_normal = 0, depth = 4, func = 0;
+    double direct[4][4], inverse[4][4];
+    double x0 = 0, y0 = 0, x1 = 0, y1 = 0, step = 0;
+};
+
+struct HostMaterial {
+    int32_t type = EMPTY;
+    double albedo[3] = {0, 0, 0};
+    double fuzz = 0, ior = 0;
+    double emit[3] = {0, 0, 0};
+};
+
+struct Scene {
+    std::vector<HostShape> shapes;
+    std::vector<HostMaterial> materials;
+    pt_camera camera;
+    double background[3];  // parsed but unused, as in the reference (src/world/mod.rs:199-202)
+};
+
+// Throws SceneError on bad input (converted to a status code at the C-ABI).
+struct SceneError {
+    int code;
+    std::string msg;
+};
+
+Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_t seed);
+
+void transform_new(const double t[3], const double r[3], const double s[3], double direct[4][4],
+                   double inverse[4][4]);
+void camera_new(const double pos[3], const double dir[3], const double up[3], double focal, double fov,
+                pt_camera *out);
+// Fills the caster part of FrameParams (pos/right/up/left_top/pixel_resolution).
+void caster_params(const pt_camera &cam, uint32_t width, uint32_t height, FrameParams *fp);
+
+// RNG spec: SplitMix64 finaliser, keyed per (pixel, sample).
+uint64_t mix64(uint64_t z);
+uint64_t sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);
+double uniform_incl_scale(double lo, double hi);
+
+DShape to_device(const HostShape &s);
+DMaterial to_device(const HostMaterial &m);
+
+}  // namespace pt

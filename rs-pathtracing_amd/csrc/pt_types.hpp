@@ -1,0 +1,44 @@
+// pt_types.hpp — device-visible layouts shared by the host library and the
+// HIP kernels.  One DShape per leaf of the realized shape list (JSON shapes in
+// file order, then the add_random_spheres spheres), 256 B each so a shape is
+// four 64-B lines; matrices keep only the three rows the kernels apply.
+#pragma once
+#include <cstdint>
+
+namespace pt {
+
+enum ShapeKind : int32_t { SPHERE = 0, RECTANGLE = 1, CUBE = 2, MARCH = 3 };
+enum MaterialKind : int32_t { LAMBERTIAN = 0, METAL = 1, DIELECTRIC = 2, DIFFUSE_LIGHT = 3, EMPTY = 4 };
+
+struct alignas(64) DShape {
+    double inv[12];  // InversableTransform::inverse, rows 0..2 (3x4)
+    double dir[12];  // InversableTransform::direct, rows 0..2
+    double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step
+    int32_t type, material, inverse_normal, depth;
+    int32_t func, pad[3];
+};
+static_assert(sizeof(DShape) == 256, "DShape is four cache lines");
+
+struct alignas(8) DMaterial {
+    int32_t type, pad;
+    double albedo[3];
+    double fuzz, ior;
+    double emit[3];
+};
+
+// Per-frame constants: MultisamplerRayCaster (src/camera/ray_caster.rs:30-48)
+// plus the tile shard this launch renders.
+struct FrameParams {
+    double pos[3], right[3], up[3], left_top[3];
+    double pixel_resolution;
+    double s11;  // UniformFloat::new_inclusive(-1, 1).scale (rand 0.8)
+    uint64_t seed;
+    uint32_t width, height, spp, depth;
+    uint32_t rank, world, tiles_x, tile_begin;
+    uint32_t tile_count, compact, pad0, pad1;
+};
+
+constexpr uint32_t TILE = 16;  // 16x16 pixels = one 256-thread workgroup
+constexpr double T_MIN = 0.001;  // ray_color: closest_hit(ray, 0.001, INF), src/renderer/mod.rs:24
+
+}  // namespace pt

@@ -25,27 +25,27 @@ METRIC = "Msamples/sec cornell_box 1920x1080x256spp at 1/2/4/8 MI355X; RMS pixel
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (FMA = 2 FLOP); no-FMA instruction peak is half of it
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
 
-# FLOPs per event of the kernel's traversal policy (counted from pt_device.hpp;
-# f64 add/sub/mul/div/sqrt = 1 each, compares and min/max not counted).
+# FLOPs per event of the kernel's own traversal (counted in pt_device.hpp /
+# pt_march.hpp; f64 add/sub/mul/div/sqrt = 1 FLOP, compares, min/max and
+# integer ops not counted).  Event counts come from the GPU itself
+# (pt_count_work, a diagnostic build of the same kernel) on a pixel sample.
 FLOP_WEIGHTS = {
-    "camera": 28,          # jittered ray + normalize
-    "leaf_xform": 33,      # inverse transform of the ray (point 18 + vector 15)
-    "sphere": 19, "rect": 4, "cube": 12, "march_bound": 31,
-    "march_step": 19,      # t += step, p += c (4) + heart_f (15)
-    "bounce": 100,         # finish(): object hit point/normal, normalisations, world transforms
-    "lambert": 20, "reject_try": 14, "metal": 25, "dielectric": 40,
+    "samples": 31,        # jittered camera ray + normalize (28), accumulate (3)
+    "bounces": 11,        # reciprocal direction (3), background on a miss (8)
+    "test_sphere": 52,    # inverse transform of the ray (33) + quadratic (19)
+    "test_rect": 37, "test_cube": 45,
+    "test_march": 64,     # transform (33) + bounding-ellipsoid quadratic (31)
+    "node_slabs": 12, "march_slabs": 12,
+    "march_steps": 19,    # t, p accumulation (4) + heart_f (15)
+    "march_tries": 45,    # interval bound of heart_f over a block's box
+    "march_blocks": 15,   # heart_f at the block end
+    "hits": 100,          # object point/normal, normalisations, world transforms
+    "lambert": 20, "metal": 25, "dielectric": 40, "reject_tries": 14, "unwind": 3,
 }
 
 
-def flops_per_sample(st):
-    w = FLOP_WEIGHTS
-    tests = sum(st["shape_tests"])
-    f = (w["camera"] * st["samples"] + w["leaf_xform"] * tests + w["sphere"] * st["shape_tests"][0]
-         + w["rect"] * st["shape_tests"][1] + w["cube"] * st["shape_tests"][2]
-         + w["march_bound"] * st["march_bounds"] + w["march_step"] * st["march_steps"]
-         + w["bounce"] * st["bounces"] + w["lambert"] * st["scatters"][0] + w["reject_try"] * st["rejection_tries"]
-         + w["metal"] * st["scatters"][1] + w["dielectric"] * st["scatters"][2])
-    return f / max(1, st["samples"])
+def flops_per_sample(cnt):
+    return sum(FLOP_WEIGHTS[k] * cnt[k] for k in FLOP_WEIGHTS) / max(1, cnt["samples"])
 
 
 def parse():
@@ -68,40 +68,35 @@ def parse():
 
 
 def cpu_baseline(text, args, threads):
-    """Oracle in the reference's BvhNode mode (the reference threaded renderer's
-    algorithm) on a bounded sample: every k-th row of the frame at 1 spp."""
+    """The oracle in the reference's BvhNode mode (the reference threaded
+    renderer's algorithm, step_by_step chunking) on a bounded sample: the full
+    frame at k spp, k chosen from a probe so the run takes ~cpu_seconds."""
     import numpy as np
     import oracle
     sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
     w, h = args.width, args.height
-    probe_rows = np.arange(0, h, max(1, h // 8))
-    px = (probe_rows[:, None] * w + np.arange(0, w, 8)[None, :]).ravel().astype(np.uint32)
+    px = (np.arange(0, h, 4)[:, None] * w + np.arange(0, w, 4)[None, :]).ravel().astype(np.uint32)
     t = time.perf_counter()
     sc.render(w, h, 1, args.depth, args.seed, pixels=px, threads=threads)
     rate = len(px) / max(1e-9, time.perf_counter() - t)
-    nrows = int(min(h, max(1, args.cpu_seconds * rate / w)))
-    stride = max(1, h // nrows)
-    rows = np.arange(stride // 2, h, stride)[:nrows]
-    px = (rows[:, None] * w + np.arange(w)[None, :]).ravel().astype(np.uint32)
+    spp = int(max(1, min(args.spp, round(args.cpu_seconds * rate / (w * h)))))
     t = time.perf_counter()
-    sc.render(w, h, 1, args.depth, args.seed, pixels=px, threads=threads)
+    sc.render(w, h, spp, args.depth, args.seed, threads=threads)
     dt = time.perf_counter() - t
-    return {"value": round(len(px) / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d full rows (every %dth) of the %dx%d frame at 1 spp, depth %d = %d samples in %.1f s; "
-                      "oracle with the reference's BvhNode traversal, step_by_step chunking"
-                      % (len(rows), stride, w, h, args.depth, len(px), dt)}
+    n = w * h * spp
+    return {"value": round(n / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "full %dx%d frame at %d spp, depth %d = %d samples in %.1f s (%d threads); oracle "
+                      "restatement with the reference's BvhNode traversal" % (w, h, spp, args.depth, n, dt, threads)}
 
 
-def algorithmic_flops(text, args):
-    """F (FLOP/sample) of the GPU kernel's policy (linear closest-hit scan, exact
-    fixed-step march), from oracle event counts on a strided pixel sample."""
+def algorithmic_flops(pt, r, cam, args):
+    """F (FLOP/sample) of the kernel's own policy, from its GPU event counters
+    on a strided pixel sample (1/144 of the frame) at 4 spp."""
     import numpy as np
-    import oracle
-    sc = oracle.Scene(text, seed=args.scene_seed)
     w, h = args.width, args.height
-    px = (np.arange(3, h, 24)[:, None] * w + np.arange(5, w, 24)[None, :]).ravel().astype(np.uint32)
-    _, st = sc.render(w, h, 2, args.depth, args.seed, pixels=px, stats=True)
-    return flops_per_sample(st), st
+    px = (np.arange(3, h, 12)[:, None] * w + np.arange(5, w, 12)[None, :]).ravel().astype(np.uint32)
+    cnt = pt.count_work(r, cam, pt.ImageParams(w, h), 4, px, seed=args.seed)
+    return flops_per_sample(cnt), cnt
 
 
 def main():
@@ -126,7 +121,8 @@ def main():
     r = pt.HipRenderer(scene, device=local, depth=args.depth)
     cam = scene.camera()
     W, H, spp = args.width, args.height, args.spp
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()  # a real stream: the HIP events below time exactly our launches
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
@@ -185,7 +181,7 @@ def main():
         threads = min(16, os.cpu_count() or 1)
 
         # roofline of the dominant kernel (render_tiles), this rank's launches
-        F, _ = algorithmic_flops(text, args)
+        F, counts = algorithmic_flops(pt, r, cam, args)
         my_tiles = pt.shard_tiles(W, H, rank, world)
         samples_launch = samples_frame * my_tiles / (pt.shard_tiles(W, H, 0, 1))
         achieved = F * samples_launch / (kernel_ms / 1e3) / 1e12
@@ -200,7 +196,8 @@ def main():
                        "parallelism": "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"},
             "roofline": {"bound": "valu_f64", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                         "flops_per_sample": round(F, 1), "kernel": "render_tiles",
+                         "flops_per_sample": round(F, 1), "kernel": "render_tiles", "events_per_sample":
+                             {k: round(v / max(1, counts["samples"]), 3) for k, v in counts.items() if k != "samples"},
                          "kernel_ms_avg": round(kernel_ms, 3), "kernel_ms_max_rank": round(kernel_ms_max, 3)},
             "roofline_hbm": {"achieved": round(out_bytes / (kernel_ms / 1e3) / 1e9, 4), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,

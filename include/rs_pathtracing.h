@@ -147,6 +147,18 @@ int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *camera, uint32_t wid
                            uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
                            double *out);
 
+/* Work counters of the kernel's own traversal policy over the listed pixels
+ * (a diagnostic build of the same path): counters[PT_NUM_COUNTERS] receives,
+ * in order, samples, bounces, sphere/rectangle/cube/marched-shape leaf tests,
+ * BVH node slabs, marched-shape box slabs, literal march steps, march jump
+ * attempts, march jumps, hits, Lambertian/Metal/Dielectric scatters,
+ * rejection-sampling tries, attenuation multiplies.  Used for the FLOP side
+ * of the roofline. */
+#define PT_NUM_COUNTERS 17
+int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                  uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
+                  uint64_t *counters);
+
 /* Display encode (src/bin/main.rs:281-289): sqrt -> clamp [0, 0.999] -> *256
  * -> u8, alpha 255; rgba is w*h*4 bytes. Host-side. */
 int pt_encode_rgba8(const double *rgb, size_t npix, uint8_t *rgba);

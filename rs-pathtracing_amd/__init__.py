@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
     "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
     "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_trace_pixel_samples", "pt_count_work", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -97,6 +97,14 @@ def lib():
         raise ImportError("%s is missing: build it with `make -C rs-pathtracing_amd` or "
                           "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)"
                           % LIB_PATH)
+    try:
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7.
+        # Loading it first lets our NEEDED libamdhip64.so.7 resolve to the same
+        # copy (same SONAME), so torch tensors / streams and our kernels share
+        # one runtime instead of two runtimes fighting over the device.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp, d = C.c_void_p, C.POINTER(C.c_double)
     u32, u64, sz = C.c_uint32, C.c_uint64, C.c_size_t
@@ -121,6 +129,8 @@ def lib():
         "pt_ray_color": (C.c_int, [vp, d, C.POINTER(u64), sz, u32, d]),
         "pt_trace_pixel_samples": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64,
                                              C.POINTER(u32), sz, d]),
+        "pt_count_work": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u32), sz,
+                                    C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
         "pt_sample_key": (u64, [u64, u64, u64]),
         "pt_last_error": (C.c_char_p, []),
@@ -308,6 +318,23 @@ class HipRenderer(Renderer):
                                             pixels.ctypes.data_as(C.POINTER(C.c_uint32)), len(pixels),
                                             _dptr(out)))
         return out
+
+
+COUNTERS = ["samples", "bounces", "test_sphere", "test_rect", "test_cube", "test_march", "node_slabs",
+            "march_slabs", "march_steps", "march_tries", "march_blocks", "hits", "lambert", "metal",
+            "dielectric", "reject_tries", "unwind"]
+
+
+def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,
+               pixels: np.ndarray, seed=None) -> dict:
+    """Event counts of the kernel's own traversal over the given pixels (pt_count_work)."""
+    pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
+    out = (C.c_uint64 * len(COUNTERS))()
+    s = renderer.seed if seed is None else int(seed)
+    _check(lib().pt_count_work(renderer._h, C.byref(camera._c), img_params.width, img_params.height,
+                               int(samples_number), s, pixels.ctypes.data_as(C.POINTER(C.c_uint32)), len(pixels),
+                               out))
+    return dict(zip(COUNTERS, list(out)))
 
 
 def shard_tiles(width: int, height: int, rank: int, world: int) -> int:

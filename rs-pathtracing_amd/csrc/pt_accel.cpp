@@ -1,0 +1,128 @@
+// pt_accel.cpp — see pt_accel.hpp.
+#include "pt_accel.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace pt {
+
+// Object-space bounds of each kind (get_bounding_box: Rectangle mod.rs:214-220,
+// Cube :295-301, Sphere :384-398, RayMarchingShape ray_marching.rs:84-91 with
+// Heart::get_bounds :174-187), transformed by the 8 corners (AABB::transform,
+// mod.rs:93-108), then padded so that every point a leaf test can return lies
+// strictly inside: 1e-7 relative + 1e-9 absolute, and for a ray-marched shape
+// two march steps more (a forward pass may overshoot `end` by one step).
+DBox shape_box(const HostShape &s) {
+    double lo[3], hi[3];
+    switch (s.type) {
+    case RECTANGLE:
+        lo[0] = s.x0; lo[1] = s.y0; lo[2] = -0.0001;
+        hi[0] = s.x1; hi[1] = s.y1; hi[2] = 0.0001;
+        break;
+    case MARCH:
+        lo[0] = -1.45; lo[1] = -(1.45 / 2.05); lo[2] = -1.45;
+        hi[0] = 1.45; hi[1] = 1.45 / 2.05; hi[2] = 1.45;
+        break;
+    default:
+        lo[0] = lo[1] = lo[2] = -1.0;
+        hi[0] = hi[1] = hi[2] = 1.0;
+    }
+    DBox b;
+    for (int k = 0; k < 3; k++) {
+        b.lo[k] = INFINITY;
+        b.hi[k] = -INFINITY;
+    }
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+            for (int k = 0; k < 2; k++) {
+                double p[3] = {i ? hi[0] : lo[0], j ? hi[1] : lo[1], k ? hi[2] : lo[2]};
+                for (int r = 0; r < 3; r++) {
+                    double v = p[0] * s.direct[r][0] + p[1] * s.direct[r][1] + p[2] * s.direct[r][2] + s.direct[r][3];
+                    b.lo[r] = std::min(b.lo[r], v);
+                    b.hi[r] = std::max(b.hi[r], v);
+                }
+            }
+    double extent = 0;
+    for (int r = 0; r < 3; r++)
+        extent = std::max({extent, std::fabs(b.lo[r]), std::fabs(b.hi[r]), b.hi[r] - b.lo[r]});
+    double pad = 1e-7 * extent + 1e-9;
+    if (s.type == MARCH) pad += 2.0 * std::fabs(s.step);
+    for (int r = 0; r < 3; r++) {
+        b.lo[r] -= pad;
+        b.hi[r] += pad;
+    }
+    return b;
+}
+
+namespace {
+
+struct Builder {
+    const std::vector<DBox> &boxes;
+    Accel &out;
+    static constexpr int LEAF = 2;
+
+    void emit(std::vector<int32_t> &ids, size_t a, size_t b) {
+        size_t me = out.nodes.size();
+        out.nodes.push_back(DNode{});
+        DNode n{};
+        for (int k = 0; k < 3; k++) {
+            n.lo[k] = INFINITY;
+            n.hi[k] = -INFINITY;
+        }
+        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t i = a; i < b; i++) {
+            const DBox &x = boxes[ids[i]];
+            for (int k = 0; k < 3; k++) {
+                n.lo[k] = std::min(n.lo[k], x.lo[k]);
+                n.hi[k] = std::max(n.hi[k], x.hi[k]);
+                double c = 0.5 * (x.lo[k] + x.hi[k]);
+                clo[k] = std::min(clo[k], c);
+                chi[k] = std::max(chi[k], c);
+            }
+        }
+        if (b - a <= (size_t)LEAF) {
+            n.first = (int32_t)out.leaf.size();
+            n.count = (int32_t)(b - a);
+            for (size_t i = a; i < b; i++) out.leaf.push_back(ids[i]);
+            n.skip = (int32_t)out.nodes.size();
+            out.nodes[me] = n;
+            return;
+        }
+        int axis = 0;
+        for (int k = 1; k < 3; k++)
+            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        size_t mid = a + (b - a) / 2;
+        std::nth_element(ids.begin() + a, ids.begin() + mid, ids.begin() + b, [&](int32_t x, int32_t y) {
+            double cx = boxes[x].lo[axis] + boxes[x].hi[axis], cy = boxes[y].lo[axis] + boxes[y].hi[axis];
+            return cx < cy || (cx == cy && x < y);
+        });
+        emit(ids, a, mid);
+        emit(ids, mid, b);
+        n.count = 0;
+        n.first = 0;
+        n.skip = (int32_t)out.nodes.size();
+        out.nodes[me] = n;
+    }
+};
+
+}  // namespace
+
+Accel build_accel(const Scene &sc, int json_shapes) {
+    Accel a;
+    a.boxes.reserve(sc.shapes.size());
+    for (auto &s : sc.shapes) a.boxes.push_back(shape_box(s));
+    std::vector<int32_t> rest;
+    bool small = json_shapes <= LIN_MAX;
+    for (int32_t i = 0; i < (int32_t)sc.shapes.size(); i++) {
+        if (sc.shapes[i].type == MARCH) a.march.push_back(i);
+        else if (small && i < json_shapes) a.lin.push_back(i);
+        else rest.push_back(i);
+    }
+    if (!rest.empty()) {
+        Builder b{a.boxes, a};
+        b.emit(rest, 0, rest.size());
+    }
+    return a;
+}
+
+}  // namespace pt

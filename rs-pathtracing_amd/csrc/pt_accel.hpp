@@ -1,0 +1,37 @@
+// pt_accel.hpp — closest-hit acceleration for the GPU path (host build).
+//
+// The reference wraps the shape list in a randomly split BvhNode tree
+// (src/world/shapes/mod.rs:620-729); its result is the ShapeCollection linear
+// minimum (mod.rs:587-596) up to exact ties.  Here the realized list is split
+// into three groups, all tested with one acceptance rule — accept t if
+// t < best or (t == best and shape index > best index) — which reproduces the
+// linear scan's "later shape wins a tie" in any visiting order:
+//   * `lin`   — the JSON shapes when there are few: a wave-uniform loop;
+//   * BVH     — everything else that is not ray-marched (random spheres,
+//               large scenes), median-split, threaded, padded f64 boxes;
+//   * `march` — ray-marched shapes, tested last behind their padded box
+//               against the best distance so far.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "pt_scene.hpp"
+#include "pt_types.hpp"
+
+namespace pt {
+
+struct Accel {
+    std::vector<DNode> nodes;
+    std::vector<int32_t> leaf;   // shape ids referenced by leaf nodes
+    std::vector<int32_t> lin;    // wave-uniform list
+    std::vector<int32_t> march;  // ray-marched shapes
+    std::vector<DBox> boxes;     // padded world AABB per shape
+};
+
+constexpr int LIN_MAX = 32;  // JSON shape count up to which the JSON shapes form `lin`
+
+Accel build_accel(const Scene &sc, int json_shapes);
+// conservative world AABB of one shape (reference get_bounding_box + padding)
+DBox shape_box(const HostShape &s);
+
+}  // namespace pt

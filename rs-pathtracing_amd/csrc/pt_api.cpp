@@ -10,9 +10,11 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rs_pathtracing.h"
+#include "pt_accel.hpp"
 #include "pt_kernel.hpp"
 #include "pt_scene.hpp"
 
@@ -179,17 +181,31 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     for (auto &s : scene->s.shapes) hs.push_back(to_device(s));
     for (auto &m : scene->s.materials) hm.push_back(to_device(m));
     if (hm.empty()) hm.push_back(DMaterial{});
+    Accel acc = build_accel(scene->s, scene->s.json_shapes);
     hipError_t err = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
-    if (err == hipSuccess) err = hipMalloc(&r->ds.shapes, hs.size() * sizeof(DShape));
-    if (err == hipSuccess) err = hipMalloc(&r->ds.mats, hm.size() * sizeof(DMaterial));
-    if (err == hipSuccess) err = hipMemcpy(r->ds.shapes, hs.data(), hs.size() * sizeof(DShape), hipMemcpyHostToDevice);
-    if (err == hipSuccess) err = hipMemcpy(r->ds.mats, hm.data(), hm.size() * sizeof(DMaterial), hipMemcpyHostToDevice);
+    auto upload = [&err](auto **dst, const auto &vec) {
+        using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+        size_t n = vec.empty() ? 1 : vec.size();
+        if (err == hipSuccess) err = hipMalloc((void **)dst, n * sizeof(T));
+        if (err == hipSuccess && !vec.empty())
+            err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice);
+    };
+    upload(&r->ds.shapes, hs);
+    upload(&r->ds.mats, hm);
+    upload(&r->ds.nodes, acc.nodes);
+    upload(&r->ds.leaf, acc.leaf);
+    upload(&r->ds.lin, acc.lin);
+    upload(&r->ds.march, acc.march);
+    upload(&r->ds.boxes, acc.boxes);
     if (err != hipSuccess) {
         pt_renderer_destroy(r);
         return hip_fail(err, "uploading the scene");
     }
     r->ds.nshapes = (int)hs.size();
     r->ds.nmats = (int)hm.size();
+    r->ds.nnodes = (int)acc.nodes.size();
+    r->ds.nlin = (int)acc.lin.size();
+    r->ds.nmarch = (int)acc.march.size();
     *out = r;
     return PT_OK;
 }
@@ -207,6 +223,11 @@ void pt_renderer_destroy(pt_renderer *r) {
     if (r->d_frame) (void)hipFree(r->d_frame);
     if (r->ds.shapes) (void)hipFree(r->ds.shapes);
     if (r->ds.mats) (void)hipFree(r->ds.mats);
+    if (r->ds.nodes) (void)hipFree(r->ds.nodes);
+    if (r->ds.leaf) (void)hipFree(r->ds.leaf);
+    if (r->ds.lin) (void)hipFree(r->ds.lin);
+    if (r->ds.march) (void)hipFree(r->ds.march);
+    if (r->ds.boxes) (void)hipFree(r->ds.boxes);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -385,6 +406,27 @@ int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *cam, uint32_t w, uin
     HIP_TRY(launch_trace_pixels(r->ds, P, dp.p, n, dout.p, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
     HIP_TRY(hipMemcpy(out, dout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_count_work(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
+                  const uint32_t *pixels, size_t n, uint64_t *counters) {
+    static_assert(C_COUNT == PT_NUM_COUNTERS, "counter list matches the header");
+    if (!r || !cam || !counters || (n && !pixels)) return fail(PT_ERR_INVALID, "null argument");
+    if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
+    for (size_t i = 0; i < n; i++)
+        if (pixels[i] >= (uint64_t)w * h) return fail(PT_ERR_INVALID, "pixel index out of range");
+    HIP_TRY(hipSetDevice(r->device));
+    FrameParams P = frame_params(r, *cam, w, h, spp, seed);
+    DevBuf<uint32_t> dp;
+    DevBuf<unsigned long long> dc;
+    HIP_TRY(dp.alloc(n));
+    HIP_TRY(dc.alloc(C_COUNT));
+    HIP_TRY(hipMemcpy(dp.p, pixels, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemsetAsync(dc.p, 0, C_COUNT * sizeof(unsigned long long), r->stream));
+    HIP_TRY(launch_count_work(r->ds, P, dp.p, n, dc.p, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(hipMemcpy(counters, dc.p, C_COUNT * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

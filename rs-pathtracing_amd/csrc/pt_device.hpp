@@ -1,14 +1,17 @@
-// pt_device.hpp — device-side math of the sample path, CDNA4 (gfx950), f64.
+// pt_device.hpp — the sample path for CDNA4 (gfx950), f64.
 //
-// Every expression keeps the Rust reference's operation order and the file is
-// compiled with -ffp-contract=off (rustc never forms an FMA), so each result is
-// the IEEE double the reference computes: f64 division and sqrt lower to
-// correctly rounded sequences on gfx950.  Citations are to the reference.
+// Every expression keeps the Rust reference's operation order and the library
+// is compiled with -ffp-contract=off (rustc never forms an FMA), so each value
+// is the IEEE double the reference computes; f64 division and sqrt lower to
+// correctly rounded sequences on gfx950.  Functions are __host__ __device__
+// only so that a test-only host build (tests/native) can check the same code
+// against the oracle on a CPU; the product runs them on the GPU only.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
+#include "pt_march.hpp"
 #include "pt_types.hpp"
 
 namespace pt {
@@ -17,56 +20,64 @@ namespace dev {
 struct V3 {
     double x, y, z;
 };
-__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // algebra/mod.rs:319-349
-__device__ __forceinline__ V3 scale(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ V3 divs(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
-__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ V3 normalize(V3 a) { return divs(a, sqrt(dot(a, a))); }  // :107-110
-__device__ __forceinline__ bool approx_zero(double a) { return fabs(a - 0.0) < 1e-15; }  // :14-17
+PT_HD V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+PT_HD V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_HD V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_HD double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // algebra/mod.rs:319-349
+PT_HD V3 scale(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+PT_HD V3 divs(V3 a, double s) { return v3(a.x / s, a.y / s, a.z / s); }
+PT_HD V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+PT_HD V3 normalize(V3 a) { return divs(a, sqrt(dot(a, a))); }  // :107-110
+PT_HD bool approx_zero(double a) { return fabs(a - 0.0) < 1e-15; }  // :14-17
 
 // --------------------------------------------------------------- RNG spec
 // SplitMix64 stream keyed by (seed, pixel, sample) — the documented stand-in
 // for rand::thread_rng; float conversions are rand 0.8's.
 constexpr uint64_t GAMMA = 0x9E3779B97F4A7C15ull;
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+PT_HD uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint64_t pixel, uint64_t sample) {
+PT_HD uint64_t sample_key(uint64_t seed, uint64_t pixel, uint64_t sample) {
     uint64_t k = mix64(seed ^ 0x6A09E667F3BCC909ull);
     k = mix64(k + (pixel + 1) * GAMMA);
     return mix64(k + (sample + 1) * 0xD1B54A32D192ED03ull);
 }
+PT_HD double bits_to_double(uint64_t b) {
+    union {
+        uint64_t u;
+        double d;
+    } x;
+    x.u = b;
+    return x.d;
+}
 struct Rng {
     uint64_t s;
-    __device__ __forceinline__ uint64_t next() {
+    PT_HD uint64_t next() {
         s += GAMMA;
         return mix64(s);
     }
     // Standard f64: (u >> 11) * 2^-53
-    __device__ __forceinline__ double gen() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
+    PT_HD double gen() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0); }
     // UniformFloat::sample: ([1,2) from 52 bits) - 1, * scale + low
-    __device__ __forceinline__ double uniform(double lo, double sc) {
-        double v = __longlong_as_double((long long)((next() >> 12) | (1023ull << 52)));
+    PT_HD double uniform(double lo, double sc) {
+        double v = bits_to_double((next() >> 12) | (1023ull << 52));
         return (v - 1.0) * sc + lo;
     }
 };
 
 // ---------------------------------------------------------- transforms
 // transform_point / transform_vector / transform_normal (algebra/transform.rs:394-425)
-__device__ __forceinline__ V3 xf_point(const double *m, V3 p) {
+PT_HD V3 xf_point(const double *m, V3 p) {
     return v3(p.x * m[0] + p.y * m[1] + p.z * m[2] + m[3], p.x * m[4] + p.y * m[5] + p.z * m[6] + m[7],
               p.x * m[8] + p.y * m[9] + p.z * m[10] + m[11]);
 }
-__device__ __forceinline__ V3 xf_vector(const double *m, V3 v) {
+PT_HD V3 xf_vector(const double *m, V3 v) {
     return v3(v.x * m[0] + v.y * m[1] + v.z * m[2], v.x * m[4] + v.y * m[5] + v.z * m[6],
               v.x * m[8] + v.y * m[9] + v.z * m[10]);
 }
-__device__ __forceinline__ V3 xf_normal(const double *m, V3 n) {
+PT_HD V3 xf_normal(const double *m, V3 n) {
     return v3(n.x * m[0] + n.y * m[4] + n.z * m[8], n.x * m[1] + n.y * m[5] + n.z * m[9],
               n.x * m[2] + n.y * m[6] + n.z * m[10]);
 }
@@ -75,7 +86,7 @@ __device__ __forceinline__ V3 xf_normal(const double *m, V3 n) {
 // Each returns true and sets *t on a hit in [min_t, max_t], object space.
 
 // Sphere::ray_intersect (shapes/mod.rs:330-374)
-__device__ __forceinline__ bool sphere_t(V3 o, V3 d, double min_t, double max_t, double *t) {
+PT_HD bool sphere_t(V3 o, V3 d, double min_t, double max_t, double *t) {
     double a = dot(d, d);
     double hb = dot(d, o);
     double c = dot(o, o) - 1.0;
@@ -96,7 +107,7 @@ __device__ __forceinline__ bool sphere_t(V3 o, V3 d, double min_t, double max_t,
     return true;
 }
 // Rectangle::ray_intersect (shapes/mod.rs:181-204)
-__device__ __forceinline__ bool rect_t(const double *p, V3 o, V3 d, double min_t, double max_t, double *t) {
+PT_HD bool rect_t(const double *p, V3 o, V3 d, double min_t, double max_t, double *t) {
     double tt = -o.z / d.z;
     if (tt < min_t || tt > max_t) return false;
     double px = o.x + d.x * tt, py = o.y + d.y * tt;
@@ -105,7 +116,7 @@ __device__ __forceinline__ bool rect_t(const double *p, V3 o, V3 d, double min_t
     return true;
 }
 // Cube::ray_intersect (shapes/mod.rs:250-285), slab on [-1, 1]^3
-__device__ __forceinline__ bool cube_t(V3 o, V3 d, double min_t, double max_t, double *t) {
+PT_HD bool cube_t(V3 o, V3 d, double min_t, double max_t, double *t) {
     double lx = (-1.0 - o.x) / d.x, ly = (-1.0 - o.y) / d.y, lz = (-1.0 - o.z) / d.z;
     double ux = (1.0 - o.x) / d.x, uy = (1.0 - o.y) / d.y, uz = (1.0 - o.z) / d.z;
     double tmin = fmax(fmax(fmax(fmin(lx, ux), fmin(ly, uy)), fmin(lz, uz)), min_t);
@@ -115,16 +126,8 @@ __device__ __forceinline__ bool cube_t(V3 o, V3 d, double min_t, double max_t, d
     return true;
 }
 
-// Heart (ray_marching.rs:121-188)
-__device__ __forceinline__ double heart_f(double px, double py, double pz) {  // :147-155
-    double x2 = px * px;
-    double y2 = py * py;
-    double z2 = pz * pz;
-    double z3 = z2 * pz;
-    double a = x2 + (9.0 / 4.0) * y2 + z2 - 1.0;
-    return a * a * a - x2 * z3 - (9.0 / 80.0) * y2 * z3;
-}
-__device__ __forceinline__ V3 heart_gradient(V3 p) {  // :157-168 (27/40 kept as in the reference)
+// Heart gradient (ray_marching.rs:157-168; the 27/40 coefficient kept as in the reference)
+PT_HD V3 heart_gradient(V3 p) {
     double a = p.x * p.x + (9.0 / 4.0) * p.y * p.y + p.z * p.z - 1.0;
     a = 3.0 * a * a;
     double z2 = p.z * p.z;
@@ -132,90 +135,101 @@ __device__ __forceinline__ V3 heart_gradient(V3 p) {  // :157-168 (27/40 kept as
     return v3(2.0 * p.x * (a - z3), (9.0 / 2.0) * p.y * (a - 0.05 * z3),
               2.0 * p.z * (a - p.z * (1.5 * p.x * p.x + (27.0 / 40.0) * p.y * p.y)));
 }
-// Heart::intersect_bound (:135-145) + solve_quadratic_equation (algebra/equation.rs:5-15)
-__device__ __forceinline__ bool heart_bound(V3 o, V3 d, double *start, double *end) {
-    const double rx = 1.45, ry = 1.45 / 2.05, rz = 1.45;
-    V3 oo = v3(o.x / rx, o.y / ry, o.z / rz), dd = v3(d.x / rx, d.y / ry, d.z / rz);
-    double a = dot(dd, dd), hb = dot(dd, oo), c = dot(oo, oo) - 1.0;
-    double disc = hb * hb - a * c;
-    if (disc < 0.0) return false;
-    double x1, x2;
-    if (disc == 0.0) {
-        x1 = -hb;
-        x2 = -hb;
-    } else {
-        double sq = sqrt(disc);
-        x1 = (-hb - sq) / a;
-        x2 = (-hb + sq) / a;
-    }
-    if (x1 < 0.0 && x2 < 0.0) return false;
-    *start = fmax(x1, 0.0);
-    *end = fmax(x2, 0.0);
-    return true;
-}
-// RayMarchingShape::ray_intersect (ray_marching.rs:20-74), exact fixed-step
-// sign-change march with `depth` refinement passes (step *= -0.01).
-__device__ __forceinline__ bool march_t(double step0, int passes, V3 o, V3 d, double min_t, double max_t,
-                                        double *t_out) {
-    double start, end;
-    if (!heart_bound(o, d, &start, &end)) return false;
-    double step = step0;
-    double t = start;
-    double px = o.x + d.x * t, py = o.y + d.y * t, pz = o.z + d.z * t;
-    double r = heart_f(px, py, pz);
-    for (int pass = 0; pass < passes; pass++) {
-        double cx = d.x * step, cy = d.y * step, cz = d.z * step;
-        bool hit = false;
-        for (;;) {
-            if (t > end || t < start) return false;
-            t += step;
-            px += cx;
-            py += cy;
-            pz += cz;
-            double next = heart_f(px, py, pz);
-            if (approx_zero(next)) {
-                hit = true;
-                break;
-            }
-            if ((r < 0.0 && next > 0.0) || (r > 0.0 && next < 0.0)) {
-                step *= -0.01;
-                r = next;
-                break;
-            }
-            r = next;
-        }
-        if (hit) break;
-    }
-    if (t < min_t || t > max_t) return false;
-    *t_out = t;
-    return true;
-}
 
 // ------------------------------------------------------------ closest hit
 struct Ray {
     V3 o, d;
 };
 
-__device__ __forceinline__ bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t) {
+template <bool STATS>
+PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct) {
     V3 o = xf_point(s.inv, r.o);  // inverse_transform_ray (transform.rs:32-37), no renormalisation
     V3 d = xf_vector(s.inv, r.d);
+    if (STATS) ct->c[C_TEST_SPHERE + s.type]++;
     switch (s.type) {
     case SPHERE: return sphere_t(o, d, min_t, max_t, t);
     case RECTANGLE: return rect_t(s.p, o, d, min_t, max_t, t);
     case CUBE: return cube_t(o, d, min_t, max_t, t);
-    default: return march_t(s.p[0], s.depth, o, d, min_t, max_t, t);
+    default: {
+        march::MarchStats ms{0, 0, 0};
+        bool h = march::heart_march<STATS>(s.p[0], s.depth, o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t, t, &ms);
+        if (STATS) {
+            ct->c[C_MARCH_STEPS] += ms.steps;
+            ct->c[C_MARCH_BLOCKS] += ms.blocks;
+            ct->c[C_MARCH_TRIES] += ms.tries;
+        }
+        return h;
+    }
     }
 }
 
-// Closest hit over the shape list: ShapeCollection semantics (shapes/mod.rs:587-596),
-// max_t shrinks to each accepted distance, later shape wins an exact tie.
-__device__ __forceinline__ int closest(const DShape *__restrict__ shapes, int n, const Ray &r, double min_t,
-                                       double max_t, double *best_t) {
+struct Scene {
+    const DShape *__restrict__ shapes;
+    const DMaterial *__restrict__ mats;
+    const DNode *__restrict__ nodes;
+    const int32_t *__restrict__ leaf;
+    const int32_t *__restrict__ lin;
+    const int32_t *__restrict__ march;
+    const DBox *__restrict__ boxes;
+    int nnodes, nlin, nmarch, pad;
+};
+
+// Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
+// far beyond the rounding of this test).
+PT_HD bool slab(const double *lo, const double *hi, const Ray &r, V3 inv, double min_t, double max_t) {
+    double tx1 = (lo[0] - r.o.x) * inv.x, tx2 = (hi[0] - r.o.x) * inv.x;
+    double ty1 = (lo[1] - r.o.y) * inv.y, ty2 = (hi[1] - r.o.y) * inv.y;
+    double tz1 = (lo[2] - r.o.z) * inv.z, tz2 = (hi[2] - r.o.z) * inv.z;
+    double tn = fmax(fmax(fmin(tx1, tx2), fmin(ty1, ty2)), fmax(fmin(tz1, tz2), min_t));
+    double tf = fmin(fmin(fmax(tx1, tx2), fmax(ty1, ty2)), fmin(fmax(tz1, tz2), max_t));
+    return tn <= tf;
+}
+
+// Closest hit with the linear scan's result (ShapeCollection, shapes/mod.rs:587-596):
+// a candidate replaces the best one if it is nearer, or equally near and later
+// in the shape list — the linear scan's "later shape wins a tie" rule, which
+// makes the visiting order (uniform list, BVH, marched shapes last) irrelevant.
+template <bool STATS = false>
+PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, double *best_t, Ctr *ct = nullptr) {
     double best = max_t;
     int who = -1;
-    for (int i = 0; i < n; i++) {
+    // wave-uniform list (few JSON shapes): scalar loads of each shape
+    for (int k = 0; k < sc.nlin; k++) {
+        int i = sc.lin[k];
         double t;
-        if (shape_test(shapes[i], r, min_t, best, &t)) {
+        if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+            best = t;
+            who = i;
+        }
+    }
+    V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    // threaded BVH over the remaining non-marched shapes
+    int n = 0;
+    while (n < sc.nnodes) {
+        const DNode &nd = sc.nodes[n];
+        if (STATS) ct->c[C_NODE_SLABS]++;
+        if (slab(nd.lo, nd.hi, r, inv, min_t, best)) {
+            for (int k = 0; k < nd.count; k++) {
+                int i = sc.leaf[nd.first + k];
+                double t;
+                if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+                    best = t;
+                    who = i;
+                }
+            }
+            n++;
+        } else {
+            n = nd.skip;
+        }
+    }
+    // ray-marched shapes last, only if their padded box is entered before `best`
+    for (int k = 0; k < sc.nmarch; k++) {
+        int i = sc.march[k];
+        const DBox &b = sc.boxes[i];
+        if (STATS) ct->c[C_MARCH_SLABS]++;
+        if (!slab(b.lo, b.hi, r, inv, min_t, best)) continue;
+        double t;
+        if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
             best = t;
             who = i;
         }
@@ -230,7 +244,7 @@ struct Hit {
 };
 // ray_hit_transformed (shapes/mod.rs:112-124): world point = direct * p_obj,
 // world normal = inverse^T * normalize(n_obj), then RayHit::set_normal (ray.rs:60-64).
-__device__ __forceinline__ Hit finish(const DShape &s, const Ray &r, double t) {
+PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
     V3 o = xf_point(s.inv, r.o);
     V3 d = xf_vector(s.inv, r.d);
     V3 p = v3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
@@ -260,26 +274,28 @@ __device__ __forceinline__ Hit finish(const DShape &s, const Ray &r, double t) {
 
 // ------------------------------------------------------------ materials
 // random_in_unit_sphere (algebra/mod.rs:77-84): rejection in [-1, 1]^3
-__device__ __forceinline__ V3 random_in_unit_sphere(Rng &rng, double s11) {
+template <bool STATS = false>
+PT_HD V3 random_in_unit_sphere(Rng &rng, double s11, Ctr *ct = nullptr) {
     for (;;) {
+        if (STATS) ct->c[C_REJECT_TRIES]++;
         double x = rng.uniform(-1.0, s11);
         double y = rng.uniform(-1.0, s11);
         double z = rng.uniform(-1.0, s11);
         if (x * x + y * y + z * z <= 1.0) return v3(x, y, z);
     }
 }
-__device__ __forceinline__ V3 reflect(V3 d, V3 n) {  // algebra/mod.rs:122-125
+PT_HD V3 reflect(V3 d, V3 n) {  // algebra/mod.rs:122-125
     V3 b = scale(n, dot(d, n));
     return sub(d, scale(b, 2.0));
 }
-__device__ __forceinline__ V3 refract(V3 d, V3 n, double ratio) {  // :127-133
+PT_HD V3 refract(V3 d, V3 n, double ratio) {  // :127-133
     double c = dot(neg(d), n);
     V3 perp = scale(add(d, scale(n, c)), ratio);
     double ps = -(sqrt(fabs(1.0 - dot(perp, perp))));
     return add(perp, scale(n, ps));
 }
 // Scene::background (src/world/mod.rs:199-202)
-__device__ __forceinline__ V3 background(V3 d) {
+PT_HD V3 background(V3 d) {
     double t = 0.5 * (d.y + 1.0);
     double u = 1.0 * (1.0 - t);
     return v3(u + 0.5 * t, u + 0.7 * t, u + 1.0 * t);
@@ -293,18 +309,18 @@ template <int NW>
 struct IdStack {
     uint64_t w[NW];
     int n;
-    __device__ __forceinline__ void clear() {
+    PT_HD void clear() {
 #pragma unroll
         for (int i = 0; i < NW; i++) w[i] = 0;
         n = 0;
     }
-    __device__ __forceinline__ void push(uint32_t id) {
+    PT_HD void push(uint32_t id) {
 #pragma unroll
         for (int i = NW - 1; i > 0; i--) w[i] = (w[i] << 32) | (w[i - 1] >> 32);
         w[0] = (w[0] << 32) | id;
         n++;
     }
-    __device__ __forceinline__ uint32_t pop() {
+    PT_HD uint32_t pop() {
         uint32_t id = (uint32_t)w[0];
 #pragma unroll
         for (int i = 0; i < NW - 1; i++) w[i] = (w[i] >> 32) | (w[i + 1] << 32);
@@ -314,73 +330,85 @@ struct IdStack {
     }
 };
 
-struct Scene {
-    const DShape *__restrict__ shapes;
-    const DMaterial *__restrict__ mats;
-    int nshapes;
-};
-
-// ray_color (src/renderer/mod.rs:23-45), iterative with exact product order.
-template <int NW>
-__device__ __forceinline__ V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s11) {
-    IdStack<NW> stk;
-    stk.clear();
-    V3 leaf;
-    for (;;) {
-        double t;
-        int who = closest(sc.shapes, sc.nshapes, ray, T_MIN, __builtin_inf(), &t);
-        if (who < 0) {
-            leaf = background(ray.d);
-            break;
-        }
-        if (depth == 0) {
-            leaf = v3(0.0, 0.0, 0.0);
-            break;
-        }
-        const DShape &s = sc.shapes[who];
-        Hit h = finish(s, ray, t);
-        const DMaterial &m = sc.mats[s.material];
-        V3 dir;
-        if (m.type == LAMBERTIAN) {  // material.rs:41-54
-            V3 u = normalize(random_in_unit_sphere(rng, s11));
-            dir = add(h.n, u);
-            if (approx_zero(dir.x) && approx_zero(dir.y) && approx_zero(dir.z)) dir = h.n;
-            stk.push((uint32_t)s.material);
-        } else if (m.type == METAL) {  // :63-76
-            V3 rf = reflect(ray.d, h.n);
-            dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere(rng, s11), m.fuzz));
-            stk.push((uint32_t)s.material);
-        } else if (m.type == DIELECTRIC) {  // :92-115
-            double ratio = h.front ? 1.0 / m.ior : m.ior;
-            double c = dot(neg(ray.d), h.n);
-            double sn = sqrt(1.0 - c * c);
-            bool refl = ratio * sn > 1.0;
-            if (!refl) {
-                double r0 = (1.0 - ratio) / (1.0 + ratio);
-                r0 = r0 * r0;
-                double x = 1.0 - c;
-                double x5 = x * ((x * x) * (x * x));  // powi(5)
-                refl = r0 + (1.0 - r0) * x5 > rng.gen();
-            }
-            dir = refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio);
-        } else {  // DiffuseLight / EmptyMaterial: no scatter, emitted()
-            leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
-            break;
-        }
-        ray.o = h.p;
-        ray.d = normalize(dir);  // Ray::new (ray.rs:12-17)
-        depth--;
+// One bounce of ray_color (src/renderer/mod.rs:23-45).  Returns true when the
+// path ends, with the leaf radiance in *leaf; otherwise advances ray/depth.
+template <int NW, bool STATS = false>
+PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng, double s11, V3 *leaf,
+                  Ctr *ct = nullptr) {
+    double t;
+    if (STATS) ct->c[C_BOUNCES]++;
+    int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
+    if (who < 0) {
+        *leaf = background(ray.d);
+        return true;
     }
-    V3 c = leaf;
+    if (depth == 0) {
+        *leaf = v3(0.0, 0.0, 0.0);
+        return true;
+    }
+    const DShape &s = sc.shapes[who];
+    if (STATS) ct->c[C_HITS]++;
+    Hit h = finish(s, ray, t);
+    const DMaterial &m = sc.mats[s.material];
+    V3 dir;
+    if (m.type == LAMBERTIAN) {  // material.rs:41-54
+        if (STATS) ct->c[C_LAMBERT]++;
+        V3 u = normalize(random_in_unit_sphere<STATS>(rng, s11, ct));
+        dir = add(h.n, u);
+        if (approx_zero(dir.x) && approx_zero(dir.y) && approx_zero(dir.z)) dir = h.n;
+        stk.push((uint32_t)s.material);
+    } else if (m.type == METAL) {  // :63-76
+        if (STATS) ct->c[C_METAL]++;
+        V3 rf = reflect(ray.d, h.n);
+        dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
+        stk.push((uint32_t)s.material);
+    } else if (m.type == DIELECTRIC) {  // :92-115
+        if (STATS) ct->c[C_DIELECTRIC]++;
+        double ratio = h.front ? 1.0 / m.ior : m.ior;
+        double c = dot(neg(ray.d), h.n);
+        double sn = sqrt(1.0 - c * c);
+        bool refl = ratio * sn > 1.0;
+        if (!refl) {
+            double r0 = (1.0 - ratio) / (1.0 + ratio);
+            r0 = r0 * r0;
+            double x = 1.0 - c;
+            double x5 = x * ((x * x) * (x * x));  // powi(5)
+            refl = r0 + (1.0 - r0) * x5 > rng.gen();
+        }
+        dir = refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio);
+    } else {  // DiffuseLight / EmptyMaterial: no scatter, emitted()
+        *leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
+        return true;
+    }
+    ray.o = h.p;
+    ray.d = normalize(dir);  // Ray::new (ray.rs:12-17)
+    depth--;
+    return false;
+}
+
+template <int NW, bool STATS = false>
+PT_HD V3 unwind(const Scene &sc, IdStack<NW> &stk, V3 c, Ctr *ct = nullptr) {
     while (stk.n > 0) {
+        if (STATS) ct->c[C_UNWIND]++;
         const DMaterial &m = sc.mats[stk.pop()];
         c = v3(m.albedo[0] * c.x, m.albedo[1] * c.y, m.albedo[2] * c.z);  // Vector3d::product
     }
     return c;
 }
 
+// ray_color (src/renderer/mod.rs:23-45), iterative with the recursion's product order.
+template <int NW>
+PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s11) {
+    IdStack<NW> stk;
+    stk.clear();
+    V3 leaf;
+    while (!bounce<NW>(sc, ray, depth, stk, rng, s11, &leaf)) {
+    }
+    return unwind<NW>(sc, stk, leaf);
+}
+
 // Camera sample: MultisamplerRayCaster::next (ray_caster.rs:103-118), u then v.
-__device__ __forceinline__ Ray camera_ray(const FrameParams &P, uint32_t x, uint32_t y, Rng &rng) {
+PT_HD Ray camera_ray(const FrameParams &P, uint32_t x, uint32_t y, Rng &rng) {
     double u = rng.gen();
     double v = rng.gen();
     double sx = P.pixel_resolution * ((double)x + u);
@@ -395,14 +423,29 @@ __device__ __forceinline__ Ray camera_ray(const FrameParams &P, uint32_t x, uint
 }
 
 // trace_pixel_samples (renderer/mod.rs:151-155): in-order sum, then / spp.
-template <int NW>
-__device__ __forceinline__ V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y) {
+// One flat loop over bounces of all the pixel's samples: a lane whose path
+// ends starts its next sample at once instead of idling until every lane of
+// the wave has finished the current one.
+template <int NW, bool STATS = false>
+PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
     V3 acc = v3(0.0, 0.0, 0.0);
-    for (uint32_t s = 0; s < P.spp; s++) {
-        Rng rng{sample_key(P.seed, pixel, s)};
-        Ray r = camera_ray(P, x, y, rng);
-        acc = add(acc, ray_color<NW>(sc, r, P.depth, rng, P.s11));
+    uint32_t s = 0;
+    Rng rng{sample_key(P.seed, pixel, 0)};
+    Ray ray = camera_ray(P, x, y, rng);
+    uint32_t depth = P.depth;
+    IdStack<NW> stk;
+    stk.clear();
+    for (;;) {
+        V3 leaf;
+        if (bounce<NW, STATS>(sc, ray, depth, stk, rng, P.s11, &leaf, ct)) {
+            acc = add(acc, unwind<NW, STATS>(sc, stk, leaf, ct));
+            if (STATS) ct->c[C_SAMPLES]++;
+            if (++s == P.spp) break;
+            rng.s = sample_key(P.seed, pixel, s);
+            ray = camera_ray(P, x, y, rng);
+            depth = P.depth;
+        }
     }
     return divs(acc, (double)P.spp);
 }

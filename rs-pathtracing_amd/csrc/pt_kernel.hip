@@ -57,7 +57,7 @@ __global__ void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays
     r.o = dev::v3(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
     r.d = dev::v3(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
     double t;
-    int who = dev::closest(sc.shapes, sc.nshapes, r, min_t, max_t, &t);
+    int who = dev::closest(sc, r, min_t, max_t, &t);
     pt_hit h = {};
     h.shape = who;
     h.material = -1;
@@ -104,8 +104,37 @@ __global__ void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t 
     out[i * 3 + 2] = c.z;
 }
 
+// Diagnostic build: the same path with per-lane event counters (STATS), summed
+// with one 64-bit atomic per counter per lane.  Only pt_count_work uses it.
+template <int NW>
+__global__ void count_work(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
+                           unsigned long long *__restrict__ ctr) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ctr c;
+    for (int k = 0; k < C_COUNT; k++) c.c[k] = 0;
+    uint32_t idx = pixels[i];
+    dev::trace_pixel<NW, true>(sc, P, idx % P.width, idx / P.width, &c);
+    for (int k = 0; k < C_COUNT; k++)
+        if (c.c[k]) atomicAdd(&ctr[k], (unsigned long long)c.c[k]);
+}
+
 // ------------------------------------------------------------- launchers
-static dev::Scene dscene(const DeviceScene &s) { return dev::Scene{s.shapes, s.mats, s.nshapes}; }
+static dev::Scene dscene(const DeviceScene &s) {
+    dev::Scene d;
+    d.shapes = s.shapes;
+    d.mats = s.mats;
+    d.nodes = s.nodes;
+    d.leaf = s.leaf;
+    d.lin = s.lin;
+    d.march = s.march;
+    d.boxes = s.boxes;
+    d.nnodes = s.nnodes;
+    d.nlin = s.nlin;
+    d.nmarch = s.nmarch;
+    d.pad = 0;
+    return d;
+}
 
 // Attenuation-stack width by depth: one 32-bit material id per bounce.
 #define PT_DISPATCH_NW(depth, CALL)        \
@@ -162,6 +191,14 @@ hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const
     if (!n) return hipSuccess;
     PT_DISPATCH_NW(P.depth, (trace_pixels_probe<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
                                 dscene(s), P, pixels, n, out)));
+    return hipGetLastError();
+}
+
+hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
+                             unsigned long long *ctr, hipStream_t st) {
+    if (!n) return hipSuccess;
+    PT_DISPATCH_NW(P.depth, (count_work<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dscene(s), P, pixels, n,
+                                                                                         ctr)));
     return hipGetLastError();
 }
 

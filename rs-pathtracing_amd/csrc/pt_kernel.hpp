@@ -10,7 +10,10 @@ namespace pt {
 struct DeviceScene {
     DShape *shapes = nullptr;
     DMaterial *mats = nullptr;
-    int nshapes = 0, nmats = 0;
+    DNode *nodes = nullptr;
+    int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
+    DBox *boxes = nullptr;
+    int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
 };
 
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st);
@@ -22,5 +25,8 @@ hipError_t launch_ray_color(const DeviceScene &s, const double *rays, uint64_t *
                             double s11, double *out, hipStream_t st);
 hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
                                double *out, hipStream_t st);
+
+hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
+                             unsigned long long *ctr, hipStream_t st);
 
 }  // namespace pt

@@ -458,6 +458,7 @@ Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_
         }
         sc.shapes.push_back(h);
     }
+    sc.json_shapes = (int)sc.shapes.size();
     if (random_spheres) add_random_spheres(sc, seed);
     if (sc.shapes.empty())  // BvhNode::new on an empty list panics (shapes/mod.rs:702-713)
         throw SceneError{PT_ERR_INVALID, "scene has no shapes"};

@@ -29,6 +29,7 @@ struct Scene {
     std::vector<HostShape> shapes;
     std::vector<HostMaterial> materials;
     pt_camera camera;
+    int json_shapes = 0;  // shapes from the JSON file; random spheres follow
     double background[3];  // parsed but unused, as in the reference (src/world/mod.rs:199-202)
 };
 

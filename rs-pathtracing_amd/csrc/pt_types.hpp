@@ -26,6 +26,19 @@ struct alignas(8) DMaterial {
     double emit[3];
 };
 
+// Threaded (skip-pointer) BVH node over shapes, DFS order: on an AABB hit go
+// to i+1 (first child, or the next node after a leaf's shapes are tested), on
+// a miss jump to `skip`.  Leaf nodes list `count` shape ids from leaf[first].
+struct alignas(64) DNode {
+    double lo[3], hi[3];
+    int32_t skip, first, count, pad;
+};
+static_assert(sizeof(DNode) == 64, "DNode is one cache line");
+
+struct DBox {
+    double lo[3], hi[3];
+};
+
 // Per-frame constants: MultisamplerRayCaster (src/camera/ray_caster.rs:30-48)
 // plus the tile shard this launch renders.
 struct FrameParams {
@@ -36,6 +49,17 @@ struct FrameParams {
     uint32_t width, height, spp, depth;
     uint32_t rank, world, tiles_x, tile_begin;
     uint32_t tile_count, compact, pad0, pad1;
+};
+
+// Work counters of the diagnostic (STATS) kernel build: the kernel's own event
+// counts, turned into algorithmic FLOPs per sample by bench.py.
+enum Counter : int {
+    C_SAMPLES, C_BOUNCES, C_TEST_SPHERE, C_TEST_RECT, C_TEST_CUBE, C_TEST_MARCH, C_NODE_SLABS, C_MARCH_SLABS,
+    C_MARCH_STEPS, C_MARCH_TRIES, C_MARCH_BLOCKS, C_HITS, C_LAMBERT, C_METAL, C_DIELECTRIC, C_REJECT_TRIES,
+    C_UNWIND, C_COUNT
+};
+struct Ctr {
+    uint64_t c[C_COUNT];
 };
 
 constexpr uint32_t TILE = 16;  // 16x16 pixels = one 256-thread workgroup

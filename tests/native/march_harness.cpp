@@ -1,0 +1,22 @@
+// Test-only host build of the product's skipping march (pt_march.hpp) so the
+// CPU suite can compare it, bit for bit, with the oracle's literal march.
+#include <cstdint>
+
+#include "../../rs-pathtracing_amd/csrc/pt_march.hpp"
+
+extern "C" int march_heart(double step, int passes, const double *inv /*3x4 row-major*/, const double *o,
+                           const double *d, double min_t, double max_t, double *t, uint32_t *steps,
+                           uint32_t *blocks) {
+    // inverse_transform_ray (transform.rs:32-37), as pt_device.hpp xf_point / xf_vector
+    double ox = o[0] * inv[0] + o[1] * inv[1] + o[2] * inv[2] + inv[3];
+    double oy = o[0] * inv[4] + o[1] * inv[5] + o[2] * inv[6] + inv[7];
+    double oz = o[0] * inv[8] + o[1] * inv[9] + o[2] * inv[10] + inv[11];
+    double dx = d[0] * inv[0] + d[1] * inv[1] + d[2] * inv[2];
+    double dy = d[0] * inv[4] + d[1] * inv[5] + d[2] * inv[6];
+    double dz = d[0] * inv[8] + d[1] * inv[9] + d[2] * inv[10];
+    pt::march::MarchStats st{0, 0, 0};
+    int hit = pt::march::heart_march<true>(step, passes, ox, oy, oz, dx, dy, dz, min_t, max_t, t, &st) ? 1 : 0;
+    *steps = st.steps;
+    *blocks = st.blocks;
+    return hit;
+}

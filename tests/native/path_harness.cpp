@@ -1,0 +1,101 @@
+// Test-only host build of the product's sample path: the same pt_device.hpp
+// functions the HIP kernels run, compiled for the CPU, on a scene realized by
+// the product's own loader and BVH builder.  Lets the CPU suite compare the
+// GPU algorithm (uniform list + threaded BVH + skipping march + flat sample
+// loop) with the oracle bit for bit.  Never used by the product.
+#include <cstring>
+#include <vector>
+
+#include "../../rs-pathtracing_amd/csrc/pt_accel.hpp"
+#include "../../rs-pathtracing_amd/csrc/pt_device.hpp"
+#include "../../rs-pathtracing_amd/csrc/pt_scene.hpp"
+
+using namespace pt;
+
+struct Bundle {
+    Scene sc;
+    Accel acc;
+    std::vector<DShape> shapes;
+    std::vector<DMaterial> mats;
+    dev::Scene view;
+    double s11;
+};
+
+extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, uint64_t seed) {
+    try {
+        Bundle *b = new Bundle;
+        b->sc = scene_from_json(json, len, random_spheres != 0, seed);
+        b->acc = build_accel(b->sc, b->sc.json_shapes);
+        for (auto &s : b->sc.shapes) b->shapes.push_back(to_device(s));
+        for (auto &m : b->sc.materials) b->mats.push_back(to_device(m));
+        b->view.shapes = b->shapes.data();
+        b->view.mats = b->mats.data();
+        b->view.nodes = b->acc.nodes.data();
+        b->view.leaf = b->acc.leaf.data();
+        b->view.lin = b->acc.lin.data();
+        b->view.march = b->acc.march.data();
+        b->view.boxes = b->acc.boxes.data();
+        b->view.nnodes = (int)b->acc.nodes.size();
+        b->view.nlin = (int)b->acc.lin.size();
+        b->view.nmarch = (int)b->acc.march.size();
+        b->s11 = uniform_incl_scale(-1.0, 1.0);
+        return b;
+    } catch (...) {
+        return nullptr;
+    }
+}
+extern "C" void h_scene_free(void *p) { delete (Bundle *)p; }
+extern "C" void h_accel_stats(void *p, int *out) {
+    Bundle *b = (Bundle *)p;
+    out[0] = (int)b->acc.nodes.size();
+    out[1] = (int)b->acc.lin.size();
+    out[2] = (int)b->acc.march.size();
+    out[3] = (int)b->acc.leaf.size();
+}
+
+extern "C" int h_closest(void *p, const double *ray, double min_t, double max_t, double *t, double *point,
+                         double *normal, int *front) {
+    Bundle *b = (Bundle *)p;
+    dev::Ray r;
+    r.o = dev::v3(ray[0], ray[1], ray[2]);
+    r.d = dev::v3(ray[3], ray[4], ray[5]);
+    int who = dev::closest(b->view, r, min_t, max_t, t);
+    if (who >= 0) {
+        dev::Hit h = dev::finish(b->shapes[who], r, *t);
+        point[0] = h.p.x, point[1] = h.p.y, point[2] = h.p.z;
+        normal[0] = h.n.x, normal[1] = h.n.y, normal[2] = h.n.z;
+        *front = h.front;
+    }
+    return who;
+}
+
+extern "C" void h_ray_color(void *p, const double *ray, uint64_t *state, uint32_t depth, double *out) {
+    Bundle *b = (Bundle *)p;
+    dev::Ray r;
+    r.o = dev::v3(ray[0], ray[1], ray[2]);
+    r.d = dev::v3(ray[3], ray[4], ray[5]);
+    dev::Rng rng{*state};
+    dev::V3 c = depth <= 8 ? dev::ray_color<4>(b->view, r, depth, rng, b->s11)
+                           : dev::ray_color<32>(b->view, r, depth, rng, b->s11);
+    *state = rng.s;
+    out[0] = c.x, out[1] = c.y, out[2] = c.z;
+}
+
+extern "C" void h_trace_pixels(void *p, uint32_t w, uint32_t h, uint32_t spp, uint32_t depth, uint64_t seed,
+                               const uint32_t *pixels, size_t n, double *out) {
+    Bundle *b = (Bundle *)p;
+    FrameParams P;
+    std::memset(&P, 0, sizeof P);
+    caster_params(b->sc.camera, w, h, &P);
+    P.s11 = b->s11;
+    P.seed = seed;
+    P.width = w;
+    P.height = h;
+    P.spp = spp;
+    P.depth = depth;
+    for (size_t i = 0; i < n; i++) {
+        dev::V3 c = depth <= 8 ? dev::trace_pixel<4>(b->view, P, pixels[i] % w, pixels[i] / w)
+                               : dev::trace_pixel<32>(b->view, P, pixels[i] % w, pixels[i] / w);
+        out[3 * i] = c.x, out[3 * i + 1] = c.y, out[3 * i + 2] = c.z;
+    }
+}

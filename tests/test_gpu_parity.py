@@ -173,3 +173,17 @@ def test_device_shards_and_unshard(pt, cornell):
     assert torch.equal(frame, full)
     host = r.render(cam, pt.ImageParams(w, h), spp, seed=3)
     assert np.array_equal(full.cpu().numpy().reshape(-1, 3), host)
+
+
+def test_count_work_diagnostic(pt, cornell):
+    """The STATS build of the kernel counts its own events and renders nothing
+    different: samples = pixels x spp, and rays aimed at the Heart march."""
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    w, h = 1920, 1080
+    pixels = np.array([560 * w + 820, 600 * w + 900, 10 * w + 10, 900 * w + 1500], np.uint32)
+    cnt = pt.count_work(r, ps.camera(), pt.ImageParams(w, h), 8, pixels, seed=3)
+    assert cnt["samples"] == 8 * len(pixels)
+    assert cnt["bounces"] >= cnt["samples"]
+    assert cnt["test_rect"] >= 6 * cnt["bounces"]  # the 6 uniform rectangles are tested every bounce
+    assert cnt["test_march"] > 0 and cnt["march_tries"] > 0

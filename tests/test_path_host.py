@@ -1,0 +1,145 @@
+"""The product's sample-path code (pt_device.hpp: uniform list + threaded BVH +
+skipping march + flat per-lane sample loop), compiled for the host by
+tests/native/Makefile, against the oracle — bit for bit, on the CPU.  The GPU
+tests repeat the comparison with the same code compiled for gfx950."""
+import ctypes as C
+import json
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+NATIVE = Path(__file__).resolve().parent / "native"
+
+
+@pytest.fixture(scope="module")
+def H():
+    subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
+    L = C.CDLL(str(NATIVE / "_build" / "libpath.so"))
+    d = C.POINTER(C.c_double)
+    L.h_scene_new.restype = C.c_void_p
+    L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]
+    L.h_scene_free.argtypes = [C.c_void_p]
+    L.h_accel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    L.h_closest.argtypes = [C.c_void_p, d, C.c_double, C.c_double, d, d, d, C.POINTER(C.c_int)]
+    L.h_ray_color.argtypes = [C.c_void_p, d, C.POINTER(C.c_uint64), C.c_uint32, d]
+    L.h_trace_pixels.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                 C.POINTER(C.c_uint32), C.c_size_t, d]
+    return L
+
+
+class Pair:
+    def __init__(self, H, text, seed=1, random_spheres=True):
+        raw = text.encode()
+        self.H = H
+        self.h = H.h_scene_new(raw, len(raw), 1 if random_spheres else 0, seed)
+        assert self.h
+        self.o = O.Scene(text, random_spheres=random_spheres, seed=seed)
+
+    def __del__(self):
+        self.H.h_scene_free(self.h)
+
+    def closest(self, ray, min_t=0.001, max_t=float("inf")):
+        t, p, n, f = C.c_double(), (C.c_double * 3)(), (C.c_double * 3)(), C.c_int()
+        who = self.H.h_closest(self.h, (C.c_double * 6)(*ray), min_t, max_t, C.byref(t), p, n, C.byref(f))
+        return who, t.value, list(p), list(n), f.value
+
+
+@pytest.fixture(scope="module")
+def cornell(H, cornell_text):
+    return Pair(H, cornell_text)
+
+
+def rays_cornell(rng, n):
+    o = rng.uniform([-20, 0, -20], [555, 555, 555], size=(n, 3))
+    o[: n // 3] = [278, 278, -800]
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # aim a third at the Heart region and a sixth at the random-sphere corner
+    k = n // 3
+    tgt = rng.uniform([140, 130, 80], [285, 270, 215], size=(k, 3))
+    d[:k] = tgt - o[:k]
+    m = n // 6
+    o[k:k + m] = rng.uniform([-30, 1, -30], [30, 5, 30], (m, 3))
+    d[k:k + m] = rng.uniform([-11, 0, -11], [11, 0.5, 11], (m, 3)) - o[k:k + m]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d], axis=1)
+
+
+def test_accel_layout(H, cornell):
+    st = (C.c_int * 4)()
+    H.h_accel_stats(cornell.h, st)
+    nodes, nlin, nmarch, nleaf = list(st)
+    assert nlin == 8 and nmarch == 1  # 6 rectangles + 2 cubes uniform; the Heart marched last
+    assert nleaf == cornell.o.num_shapes - 9  # every random sphere sits in the BVH once
+
+
+def test_closest_hit_matches_oracle(cornell):
+    rng = np.random.default_rng(21)
+    for ray in rays_cornell(rng, 3000):
+        who, t, p, n, f = cornell.closest(ray)
+        h = cornell.o.closest_hit(ray[:3], ray[3:])
+        if h is None:
+            assert who == -1
+        else:
+            assert (who, t, p, n, f) == (h.shape, h.t, list(h.point), list(h.normal), h.front_face), ray
+
+
+def test_closest_hit_max_t(cornell):
+    rng = np.random.default_rng(2)
+    for ray in rays_cornell(rng, 300):
+        for max_t in (200.0, 900.0):
+            who, t, *_ = cornell.closest(ray, 0.001, max_t)
+            h = cornell.o.closest_hit(ray[:3], ray[3:], 0.001, max_t)
+            assert (who, t if who >= 0 else None) == ((h.shape, h.t) if h else (-1, None))
+
+
+def test_ray_color_matches_oracle(H, cornell):
+    rng = np.random.default_rng(8)
+    out = (C.c_double * 3)()
+    for i, ray in enumerate(rays_cornell(rng, 600)):
+        st = C.c_uint64(int(rng.integers(0, 2 ** 63)))
+        s0 = st.value
+        H.h_ray_color(cornell.h, (C.c_double * 6)(*ray), C.byref(st), 8, out)
+        want, s1 = cornell.o.ray_color(ray[:3], ray[3:], 8, s0)
+        assert list(out) == list(want) and st.value == s1
+
+
+@pytest.mark.parametrize("scene,depth,seed", [("cornell_box.json", 8, 1), ("spheres.json", 50, 3),
+                                              ("cornell_box.json", 0, 2)])
+def test_trace_pixels_match_oracle(H, scene, depth, seed):
+    from conftest import scene_text
+    pr = Pair(H, scene_text(scene), seed=seed)
+    w, h = 1920, 1080
+    rng = np.random.default_rng(seed)
+    px = rng.choice(w * h, size=120, replace=False).astype(np.uint32)
+    out = np.zeros((len(px), 3))
+    H.h_trace_pixels(pr.h, w, h, 2, depth, seed, px.ctypes.data_as(C.POINTER(C.c_uint32)), len(px),
+                     out.ctypes.data_as(C.POINTER(C.c_double)))
+    ref = pr.o.render(w, h, 2, depth, seed, pixels=px)
+    assert np.array_equal(out, ref)
+
+
+def test_many_json_shapes_go_to_bvh(H):
+    """Above LIN_MAX JSON shapes everything non-marched is in the BVH (config C5)."""
+    shapes = [{"type": "Sphere", "name": "S%d" % i, "material": "M",
+               "transform": {"translate": [i % 7 - 3.0, 0.3 * (i // 7), 5.0 + i * 0.01], "rotate": [0, 0, 0],
+                             "scale": [0.2, 0.2, 0.2]}} for i in range(60)]
+    js = {"camera": {"position": [0, 0, -5], "direction": [0, 0, 1], "up": [0, 1, 0], "fov": 60, "focal_length": 1},
+          "shapes": shapes, "materials": {"M": {"type": "Metal", "albedo": {"type": "SolidColor", "color": [0.8, 0.7, 0.6]},
+                                                "fuzz": 0.2}}, "background": [0, 0, 0]}
+    pr = Pair(H, json.dumps(js), random_spheres=False)
+    st = (C.c_int * 4)()
+    H.h_accel_stats(pr.h, st)
+    assert st[1] == 0 and st[3] == 60
+    rng = np.random.default_rng(4)
+    for _ in range(500):
+        o = rng.uniform([-4, -1, -6], [4, 4, -4])
+        d = rng.uniform([-4, -1, 4], [4, 4, 6]) - o
+        d /= np.linalg.norm(d)
+        who, t, *_ = pr.closest(np.concatenate([o, d]))
+        h = pr.o.closest_hit(o, d)
+        assert (who, t if who >= 0 else None) == ((h.shape, h.t) if h else (-1, None))

@@ -341,6 +341,30 @@ def shard_tiles(width: int, height: int, rank: int, world: int) -> int:
     return lib().pt_shard_tiles(width, height, rank, world)
 
 
+def shard_pixels(width: int, height: int, rank: int, world: int) -> np.ndarray:
+    """Pixel index (x + y*w) of each slot of rank's compact shard, -1 outside
+    the frame: tile k (16x16, row-major tiles) belongs to rank k % world, tiles
+    in order, pixels row-major inside a tile (render_tiles' layout)."""
+    tx = (width + TILE - 1) // TILE
+    ty = (height + TILE - 1) // TILE
+    k = np.arange(rank, tx * ty, world)
+    ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
+    x = (k % tx)[:, None] * TILE + lx[None, :]
+    y = (k // tx)[:, None] * TILE + ly[None, :]
+    idx = np.where((x < width) & (y < height), y * width + x, -1)
+    return idx.ravel()
+
+
+def unshard_host(gathered: np.ndarray, width: int, height: int, world: int) -> np.ndarray:
+    """Host mirror of pt_unshard_device: (world, per*256, 3) shards -> (w*h, 3) frame."""
+    frame = np.zeros((width * height, 3), dtype=gathered.dtype)
+    for rank in range(world):
+        idx = shard_pixels(width, height, rank, world)
+        ok = idx >= 0
+        frame[idx[ok]] = gathered[rank, : len(idx)][ok]
+    return frame
+
+
 def unshard_device(gathered_ptr: int, width: int, height: int, world: int, frame_ptr: int, stream_ptr: int = 0):
     _check(lib().pt_unshard_device(C.c_void_p(gathered_ptr), width, height, world, C.c_void_p(frame_ptr),
                                    C.c_void_p(stream_ptr)))

@@ -11,13 +11,21 @@
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
 
+#include <cstdlib>
+
+#ifndef PT_DEFAULT_WAVES
+#define PT_DEFAULT_WAVES 2
+#endif
+
 namespace pt {
 
 using dev::Ray;
 using dev::V3;
 
-template <int NW>
-__global__ __launch_bounds__(256) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
+// WAVES = minimum waves per SIMD the register allocation must allow
+// (__launch_bounds__' second argument): 2 -> <= 256 VGPRs, 3 -> <= 168, 4 -> <= 128.
+template <int NW, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
     const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
     const uint32_t k = P.rank + ti * P.world;       // global tile id
     const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
@@ -49,7 +57,7 @@ __global__ void unshard(const double *__restrict__ g, uint32_t width, uint32_t h
     frame[i * 3 + 2] = s[2];
 }
 
-__global__ void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays, size_t n, double min_t,
+__global__ __launch_bounds__(256) void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays, size_t n, double min_t,
                                   double max_t, pt_hit *__restrict__ out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -77,7 +85,7 @@ __global__ void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays
 }
 
 template <int NW>
-__global__ void ray_color_probe(dev::Scene sc, const double *__restrict__ rays, uint64_t *__restrict__ states,
+__global__ __launch_bounds__(256) void ray_color_probe(dev::Scene sc, const double *__restrict__ rays, uint64_t *__restrict__ states,
                                 size_t n, uint32_t depth, double s11, double *__restrict__ out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -93,7 +101,7 @@ __global__ void ray_color_probe(dev::Scene sc, const double *__restrict__ rays, 
 }
 
 template <int NW>
-__global__ void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
+__global__ __launch_bounds__(256) void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
                                    double *__restrict__ out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -107,7 +115,7 @@ __global__ void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t 
 // Diagnostic build: the same path with per-lane event counters (STATS), summed
 // with one 64-bit atomic per counter per lane.  Only pt_count_work uses it.
 template <int NW>
-__global__ void count_work(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
+__global__ __launch_bounds__(256) void count_work(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
                            unsigned long long *__restrict__ ctr) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -154,9 +162,29 @@ static dev::Scene dscene(const DeviceScene &s) {
         }                                  \
     } while (0)
 
+// Occupancy variant of render_tiles (PT_WAVES=2|3|4 in the environment, read
+// once; default below).  Depths > 8 use the 2-wave build: their attenuation
+// stacks are wider.
+static int render_waves() {
+    static int w = [] {
+        const char *e = getenv("PT_WAVES");
+        int v = e ? atoi(e) : PT_DEFAULT_WAVES;
+        return (v >= 2 && v <= 4) ? v : PT_DEFAULT_WAVES;
+    }();
+    return w;
+}
+
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st) {
     if (P.tile_count == 0) return hipSuccess;
-    PT_DISPATCH_NW(P.depth, (render_tiles<NW><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out)));
+    if (P.depth <= 8) {
+        switch (render_waves()) {
+        case 2: render_tiles<4, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        case 3: render_tiles<4, 3><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        default: render_tiles<4, 4><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        }
+    } else {
+        PT_DISPATCH_NW(P.depth, (render_tiles<NW, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out)));
+    }
     return hipGetLastError();
 }
 

@@ -104,7 +104,12 @@ PT_HD int64_t lin_init(double x, double c, Lin *L) {
     L->R = R;
     L->sh = e - 52;
     if (Rs == 0) return BIG;
-    int64_t room = Rs > 0 ? (hi - A) / Rs : (A - lo) / (-Rs);
+    // room = floor(span / |Rs|) without a (software) int64 division: both are
+    // integers < 2^53, exact in f64; the rounded quotient is off by at most one.
+    int64_t span = Rs > 0 ? hi - A : A - lo, step = Rs > 0 ? Rs : -Rs;
+    int64_t room = (int64_t)floor((double)span / (double)step);
+    if (room * step > span) room--;
+    else if ((room + 1) * step <= span) room++;
     return room + 1 < BIG ? room + 1 : BIG;
 }
 

@@ -10,14 +10,15 @@
 //     is an integer multiple of u = 2^(e-52), so fl(x + c) = x + R*u with
 //     R = rint(c/u), as long as x + c stays in the binade and c/u is not a
 //     round-half-even tie.  With X = x/u an exact int64, B repeated additions
-//     are X + B*R: exact, O(1).  Blocks stop where any of px, py, pz, t would
-//     leave its binade; a tie or a coordinate near 0 falls back to one
-//     literal step.
-//  2. Sign proof.  Over the axis-aligned box spanned by p_k .. p_{k+B} (each
-//     coordinate is monotone), interval arithmetic bounds heart_f; if the bound
-//     keeps the sign of r with a margin covering f64 evaluation error plus the
-//     1e-15 approx_equal threshold, none of the B steps can stop the pass, so
-//     the march jumps to p_{k+B} and evaluates f there exactly.
+//     are X + B*R: exact, O(1) (a round-half-even tie is exact too, from an
+//     even X).  Blocks stop where any of px, py, pz, t would leave its binade;
+//     a coordinate near 0 falls back to one literal step.
+//  2. Sign proof.  Within such a block the step points are exactly
+//     p_j = p_k + j*ch, so heart_f along them is an exact degree-6 polynomial
+//     in j.  Its Taylor coefficients, with a rigorous bound on every rounding
+//     error (coefficients and the reference's own evaluation) plus the 1e-15
+//     approx_equal threshold, prove when none of the B steps can stop the
+//     pass; the march then jumps to p_{k+B} and evaluates f there exactly.
 // Everything else (range checks, pass structure, final t test) is the
 // reference's.  Compiled with -ffp-contract=off.
 #pragma once
@@ -92,10 +93,19 @@ PT_HD int64_t lin_init(double x, double c, Lin *L) {
     if (e < -960) return 0;  // stay clear of subnormals
     double q = ldexp(c, 52 - e);  // c / u, exact (power-of-two scaling)
     if (!(fabs(q) < 4.0e15)) return 0;  // |c| >= 2^52 u: leaves the binade at once
-    double qr = rint(q);
-    if (fabs(q - qr) == 0.5) return 0;  // round-half-even tie: depends on x's last bit
     int64_t X = (int64_t)ldexp(x, 52 - e);
-    int64_t R = (int64_t)qr;
+    double qf = floor(q);
+    int64_t R;
+    if (q - qf == 0.5) {
+        // Round-half-even tie: x + c sits halfway between two grid points and
+        // rounds to the even one.  From an even X the sum lands on an even X
+        // again, advancing by the even one of {k, k+1} every step.
+        if (X & 1) return 0;  // one literal step first makes X even
+        int64_t k = (int64_t)qf;
+        R = (k & 1) ? k + 1 : k;
+    } else {
+        R = (int64_t)rint(q);
+    }
     int64_t C = (int64_t)ceil(fabs(q));
     const int64_t lo = ((int64_t)1 << 52) + C + 1, hi = ((int64_t)1 << 53) - C - 1;
     int64_t A = X >= 0 ? X : -X, Rs = X >= 0 ? R : -R;
@@ -118,55 +128,65 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
     return ldexp((double)(L.X + j * L.R), L.sh);
 }
 
-// ------------------------------------------------------- interval bound
-PT_HD void isq(double lo, double hi, double *a, double *b) {
-    if (lo >= 0.0) {
-        *a = lo * lo;
-        *b = hi * hi;
-    } else if (hi <= 0.0) {
-        *a = hi * hi;
-        *b = lo * lo;
-    } else {
-        *a = 0.0;
-        *b = fmax(lo * lo, hi * hi);
+// ------------------------------------------------ polynomial sign proof
+// Inside a block every coordinate advances by an exact constant (R*u), so the
+// step points are exactly p_j = p0 + j*ch (ch = per-step displacement, exact),
+// and heart_f along them is the degree-6 polynomial g(j) = f(p0 + j*ch) of the
+// exact arithmetic.  heart_poly computes its coefficients; the bound below
+// proves that every f64 evaluation of heart_f at p_1..p_B keeps one sign and
+// stays clear of the 1e-15 stop.
+struct Poly {
+    double g[7];                       // coefficients of g(j)
+    double ax, ay, az, cx, cy, cz;     // |p0|, |ch| for the magnitude bound
+};
+
+PT_HD void heart_poly(double x, double y, double z, double cx, double cy, double cz, Poly *P) {
+    double x2[3] = {x * x, 2.0 * x * cx, cx * cx};
+    double y2[3] = {y * y, 2.0 * y * cy, cy * cy};
+    double z2[3] = {z * z, 2.0 * z * cz, cz * cz};
+    double z3[4] = {z2[0] * z, z2[0] * cz + z2[1] * z, z2[1] * cz + z2[2] * z, z2[2] * cz};
+    double A[3] = {x2[0] + 2.25 * y2[0] + z2[0] - 1.0, x2[1] + 2.25 * y2[1] + z2[1], x2[2] + 2.25 * y2[2] + z2[2]};
+    double A2[5] = {A[0] * A[0], 2.0 * A[0] * A[1], A[1] * A[1] + 2.0 * A[0] * A[2], 2.0 * A[1] * A[2], A[2] * A[2]};
+    double A3[7];
+    A3[0] = A2[0] * A[0];
+    A3[1] = A2[0] * A[1] + A2[1] * A[0];
+    A3[2] = A2[0] * A[2] + A2[1] * A[1] + A2[2] * A[0];
+    A3[3] = A2[1] * A[2] + A2[2] * A[1] + A2[3] * A[0];
+    A3[4] = A2[2] * A[2] + A2[3] * A[1] + A2[4] * A[0];
+    A3[5] = A2[3] * A[2] + A2[4] * A[1];
+    A3[6] = A2[4] * A[2];
+    const double K = 9.0 / 80.0;  // the reference's constant, as rounded
+    for (int k = 0; k < 7; k++) {
+        double pk = 0.0, qk = 0.0;
+        for (int i = 0; i < 3; i++) {
+            int j = k - i;
+            if (j >= 0 && j < 4) {
+                pk += x2[i] * z3[j];
+                qk += y2[i] * z3[j];
+            }
+        }
+        P->g[k] = A3[k] - pk - K * qk;
     }
-}
-// [a] (a >= 0) times [b]
-PT_HD void imulpos(double alo, double ahi, double blo, double bhi, double *lo, double *hi) {
-    if (blo >= 0.0) {
-        *lo = alo * blo;
-        *hi = ahi * bhi;
-    } else if (bhi <= 0.0) {
-        *lo = ahi * blo;
-        *hi = alo * bhi;
-    } else {
-        *lo = ahi * blo;
-        *hi = ahi * bhi;
-    }
+    P->ax = fabs(x);
+    P->ay = fabs(y);
+    P->az = fabs(z);
+    P->cx = fabs(cx);
+    P->cy = fabs(cy);
+    P->cz = fabs(cz);
 }
 
-// True if every f64 evaluation of heart_f at a point of the box has the sign
-// of `sgn` and magnitude >= 1e-15 (so neither the approx_equal stop nor a
-// sign change can fire).
-PT_HD bool heart_sign_definite(double xlo, double xhi, double ylo, double yhi, double zlo, double zhi,
-                               double sgn) {
-    double x2l, x2h, y2l, y2h, z2l, z2h;
-    isq(xlo, xhi, &x2l, &x2h);
-    isq(ylo, yhi, &y2l, &y2h);
-    isq(zlo, zhi, &z2l, &z2h);
-    double z3l = zlo * zlo * zlo, z3h = zhi * zhi * zhi;
-    double al = x2l + 2.25 * y2l + z2l - 1.0, ah = x2h + 2.25 * y2h + z2h - 1.0;
-    double a3l = al * al * al, a3h = ah * ah * ah;
-    double pl, ph, ql, qh;
-    imulpos(x2l, x2h, z3l, z3h, &pl, &ph);
-    imulpos(y2l, y2h, z3l, z3h, &ql, &qh);
-    double fl = a3l - ph - 0.1125 * qh;
-    double fh = a3h - pl - 0.1125 * ql;
-    double aa = fmax(fabs(al), fabs(ah));
-    double z3a = fmax(fabs(z3l), fabs(z3h));
-    double s = aa * aa * aa + x2h * z3a + 0.1125 * y2h * z3a + 3.0 * aa * aa * (x2h + 2.25 * y2h + z2h + 1.0);
-    double m = 1e-15 + 1e-14 * s;  // >= 90 ulp-factors of the evaluation error
-    return sgn > 0.0 ? fl > m : fh < -m;
+// True if sgn * g(j) exceeds every rounding error and the 1e-15 stop for all
+// j in [1, b]: sgn*g0 - sum_k |g_k| b^k > 1e-15 + 128 eps M(b), where M(b) bounds
+// the magnitudes of all monomials over the block (it covers both the error of
+// the coefficients above and that of the reference's own f64 evaluation).
+PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
+    double d = 0.0;
+    for (int k = 6; k >= 1; k--) d = (d + fabs(P.g[k])) * b;
+    double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
+    double x2 = xm * xm, y2 = ym * ym, z2 = zm * zm, z3 = z2 * zm;
+    double am = x2 + 2.25 * y2 + z2 + 1.0;
+    double m = am * am * am + x2 * z3 + 0.1125 * y2 * z3;
+    return sgn * P.g[0] - d > 1e-15 + 1.4210854715202004e-14 * m;  // 128 * 2^-53
 }
 
 // ------------------------------------------------------- the march
@@ -185,47 +205,52 @@ PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz
     double t = start;
     double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
     double r = heart_f(px, py, pz);
-    int64_t btry = 64;
     bool hit = false;
     for (int pass = 0; pass < passes && !hit; pass++) {
         double cx = dx * s, cy = dy * s, cz = dz * s;
         for (;;) {
             if (t > end || t < start) return false;
-            // ---- try to jump a block of B steps
+            // ---- try to jump a block of b steps (exact closed form + sign proof)
             if (r != 0.0) {
                 Lin Lx, Ly, Lz, Lt;
                 int64_t bmax = lin_init(px, cx, &Lx);
                 if (bmax >= 2) bmax = imin(bmax, lin_init(py, cy, &Ly));
                 if (bmax >= 2) bmax = imin(bmax, lin_init(pz, cz, &Lz));
                 if (bmax >= 2) bmax = imin(bmax, lin_init(t, s, &Lt));
-                int64_t b = imin(bmax, btry);
-                bool jumped = false;
-                while (b >= 2) {
+                bmax = imin(bmax, (int64_t)1 << 24);
+                if (bmax >= 2) {
+                    // exact per-step displacement of each coordinate
+                    double hx = Lx.frozen ? 0.0 : ldexp((double)Lx.R, Lx.sh);
+                    double hy = Ly.frozen ? 0.0 : ldexp((double)Ly.R, Ly.sh);
+                    double hz = Lz.frozen ? 0.0 : ldexp((double)Lz.R, Lz.sh);
+                    Poly P;
+                    heart_poly(px, py, pz, hx, hy, hz, &P);
                     if (STATS) st->tries++;
-                    double tl = lin_at(Lt, t, b - 1);  // t before the last step of the block
-                    if (tl > end || tl < start) {
+                    // first guess from the linear term, then halve until proven
+                    double sgn = r > 0.0 ? 1.0 : -1.0;
+                    double lead = sgn * P.g[0], slope = fabs(P.g[1]);
+                    int64_t b = bmax;
+                    if (slope > 0.0 && lead > 0.0) {
+                        double est = lead / slope;
+                        if (est < (double)b) b = est < 2.0 ? 2 : (int64_t)est;
+                    }
+                    bool jumped = false;
+                    while (b >= 2) {
+                        double tl = lin_at(Lt, t, b - 1);  // t before the last step of the block
+                        if (!(tl > end || tl < start) && poly_sign_definite(P, (double)b, sgn)) {
+                            t = lin_at(Lt, t, b);
+                            px = lin_at(Lx, px, b);
+                            py = lin_at(Ly, py, b);
+                            pz = lin_at(Lz, pz, b);
+                            r = heart_f(px, py, pz);
+                            if (STATS) st->blocks++;
+                            jumped = true;
+                            break;
+                        }
                         b >>= 1;
-                        continue;
                     }
-                    double qx = lin_at(Lx, px, b), qy = lin_at(Ly, py, b), qz = lin_at(Lz, pz, b);
-                    if (heart_sign_definite(fmin(px, qx), fmax(px, qx), fmin(py, qy), fmax(py, qy), fmin(pz, qz),
-                                            fmax(pz, qz), r)) {
-                        t = lin_at(Lt, t, b);
-                        px = qx;
-                        py = qy;
-                        pz = qz;
-                        r = heart_f(px, py, pz);
-                        if (STATS) st->blocks++;
-                        jumped = true;
-                        break;
-                    }
-                    b >>= 1;
+                    if (jumped) continue;
                 }
-                if (jumped) {
-                    btry = imin(b * 2, (int64_t)1 << 20);
-                    continue;
-                }
-                btry = 4;
             }
             // ---- one literal step (ray_marching.rs:38-51)
             t += s;
@@ -241,7 +266,6 @@ PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz
             if ((r < 0.0 && next > 0.0) || (r > 0.0 && next < 0.0)) {
                 s *= -0.01;
                 r = next;
-                btry = 8;
                 break;
             }
             r = next;

@@ -18,5 +18,6 @@ extern "C" int march_heart(double step, int passes, const double *inv /*3x4 row-
     int hit = pt::march::heart_march<true>(step, passes, ox, oy, oz, dx, dy, dz, min_t, max_t, t, &st) ? 1 : 0;
     *steps = st.steps;
     *blocks = st.blocks;
+    steps[1] = st.tries;
     return hit;
 }

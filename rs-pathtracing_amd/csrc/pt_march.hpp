@@ -128,6 +128,41 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
     return ldexp((double)(L.X + j * L.R), L.sh);
 }
 
+// x after n literal additions fl(x + c), exactly, across any number of binade
+// edges: closed form inside each binade, literal adds in the thin zone at an
+// edge (and near zero).  Each coordinate's sequence is independent of the
+// others, so p, t can be advanced separately.
+PT_HD double advance(double x, double c, int64_t n) {
+    while (n > 0) {
+        Lin L;
+        int64_t room = lin_init(x, c, &L);
+        if (room >= 2) {
+            int64_t k = room < n ? room : n;
+            x = lin_at(L, x, k);
+            n -= k;
+        } else {
+            x = x + c;
+            n--;
+        }
+    }
+    return x;
+}
+
+// Largest b (<= cap) such that t_0 .. t_{b-1} of t_{j+1} = fl(t_j + s) all lie
+// in [start, end] (the reference's check before each step), given t_0 does.
+PT_HD int64_t steps_in_range(double t, double s, double start, double end, int64_t cap) {
+    double lim = s > 0.0 ? end : start;
+    double est = (lim - t) / s;  // >= 0
+    int64_t k = est >= (double)cap ? cap : (int64_t)est;  // candidate last index
+    auto inside = [&](int64_t j) {
+        double tj = advance(t, s, j);
+        return !(tj > end || tj < start);
+    };
+    while (k > 0 && !inside(k)) k--;
+    while (k + 1 < cap && inside(k + 1)) k++;
+    return k + 1;
+}
+
 // ------------------------------------------------ polynomial sign proof
 // Inside a block every coordinate advances by an exact constant (R*u), so the
 // step points are exactly p_j = p0 + j*ch (ch = per-step displacement, exact),
@@ -175,18 +210,65 @@ PT_HD void heart_poly(double x, double y, double z, double cx, double cy, double
     P->cz = fabs(cz);
 }
 
-// True if sgn * g(j) exceeds every rounding error and the 1e-15 stop for all
-// j in [1, b]: sgn*g0 - sum_k |g_k| b^k > 1e-15 + 128 eps M(b), where M(b) bounds
-// the magnitudes of all monomials over the block (it covers both the error of
-// the coefficients above and that of the reference's own f64 evaluation).
-PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
-    double d = 0.0;
-    for (int k = 6; k >= 1; k--) d = (d + fabs(P.g[k])) * b;
+// True if sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither
+// the approx_equal stop nor a sign change can fire inside the block).
+//  * margin: 1e-15 + 256 eps M(b), where M(b) bounds the magnitudes of all
+//    monomials over the block; it covers the coefficients' rounding, the
+//    Horner evaluation below and the reference's own f64 evaluation of f.
+//  * monotone form: if |g1| exceeds the derivative's other terms over [0, b]
+//    (with the same kind of margin), g is monotone there and its extreme on
+//    [1, b] is g(b) (decreasing) or at least g(0) (increasing);
+//  * otherwise the absolute Taylor bound g0 - sum_k |g_k| b^k.
+PT_HD double poly_mag(const Poly &P, double b) {
     double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
     double x2 = xm * xm, y2 = ym * ym, z2 = zm * zm, z3 = z2 * zm;
     double am = x2 + 2.25 * y2 + z2 + 1.0;
-    double m = am * am * am + x2 * z3 + 0.1125 * y2 * z3;
-    return sgn * P.g[0] - d > 1e-15 + 1.4210854715202004e-14 * m;  // 128 * 2^-53
+    return am * am * am + x2 * z3 + 0.1125 * y2 * z3;
+}
+
+PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
+    const double e256 = 2.8421709430404007e-14;  // 256 * 2^-53
+    double mag = poly_mag(P, b);
+    // The step points are p_j = p0 + j*c + delta_j with |delta_j,k| <= j*ulp_k/2
+    // (each literal add rounds once): add max|grad f| . |delta| over the block.
+    double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
+    double x2 = xm * xm, y2 = ym * ym, z2 = zm * zm, z3 = z2 * zm;
+    double am = x2 + 2.25 * y2 + z2 + 1.0, am2 = am * am;
+    double gx = 6.0 * xm * am2 + 2.0 * xm * z3;
+    double gy = 13.5 * ym * am2 + 0.225 * ym * z3;
+    double gz = 6.0 * zm * am2 + 3.0 * x2 * z2 + 0.3375 * y2 * z2;
+    double drift = b * 2.3e-16 * (gx * xm + gy * ym + gz * zm);  // ulp(v)/2 <= 2^-53 |v| (2.3e-16 > 2^-52)
+    double margin = 1e-15 + e256 * mag + drift;
+    double g0 = sgn * P.g[0], g1 = sgn * P.g[1];
+    if (g0 <= margin) return false;
+    // derivative remainder sum_{k>=2} k |g_k| b^(k-1)
+    double d1 = 0.0;
+    for (int k = 6; k >= 2; k--) d1 = d1 * b + k * fabs(P.g[k]);
+    d1 *= b;
+    if (fabs(g1) - d1 > e256 * 6.0 * mag / b) {
+        if (g1 > 0.0) return true;  // increasing away from zero: min is g(0+) > g0 > margin
+        double gb = 0.0;            // decreasing: the minimum is g(b)
+        for (int k = 6; k >= 0; k--) gb = gb * b + sgn * P.g[k];
+        return gb > margin;
+    }
+    double d = 0.0;
+    for (int k = 6; k >= 1; k--) d = (d + fabs(P.g[k])) * b;
+    return g0 - d > margin;
+}
+
+// Predicted first crossing (in steps) from the quadratic part of sgn*g; the
+// search starts there and the proof decides.
+PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
+    double L = sgn * P.g[0], S = sgn * P.g[1], Q = sgn * P.g[2];
+    if (L <= 0.0) return 1.0;
+    if (Q == 0.0) return S < 0.0 ? fmin(cap, L / -S) : cap;
+    double disc = S * S - 4.0 * Q * L;
+    if (disc < 0.0) return cap;  // no real root of the quadratic
+    double sq = sqrt(disc);
+    double r1 = (-S - sq) / (2.0 * Q), r2 = (-S + sq) / (2.0 * Q);
+    double lo = fmin(r1, r2), hi = fmax(r1, r2);
+    double r = lo > 0.0 ? lo : (hi > 0.0 ? hi : cap);
+    return fmin(cap, r);
 }
 
 // ------------------------------------------------------- the march
@@ -210,46 +292,36 @@ PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz
         double cx = dx * s, cy = dy * s, cz = dz * s;
         for (;;) {
             if (t > end || t < start) return false;
-            // ---- try to jump a block of b steps (exact closed form + sign proof)
+            // ---- try to jump a block of b steps (exact advance + sign proof)
             if (r != 0.0) {
-                Lin Lx, Ly, Lz, Lt;
-                int64_t bmax = lin_init(px, cx, &Lx);
-                if (bmax >= 2) bmax = imin(bmax, lin_init(py, cy, &Ly));
-                if (bmax >= 2) bmax = imin(bmax, lin_init(pz, cz, &Lz));
-                if (bmax >= 2) bmax = imin(bmax, lin_init(t, s, &Lt));
-                bmax = imin(bmax, (int64_t)1 << 24);
+                int64_t bmax = steps_in_range(t, s, start, end, (int64_t)1 << 24);
                 if (bmax >= 2) {
-                    // exact per-step displacement of each coordinate
-                    double hx = Lx.frozen ? 0.0 : ldexp((double)Lx.R, Lx.sh);
-                    double hy = Ly.frozen ? 0.0 : ldexp((double)Ly.R, Ly.sh);
-                    double hz = Lz.frozen ? 0.0 : ldexp((double)Lz.R, Lz.sh);
                     Poly P;
-                    heart_poly(px, py, pz, hx, hy, hz, &P);
+                    heart_poly(px, py, pz, cx, cy, cz, &P);
                     if (STATS) st->tries++;
-                    // first guess from the linear term, then halve until proven
+                    // largest provable block: start at the predicted crossing,
+                    // gallop up while proven, then bisect between proven / not
                     double sgn = r > 0.0 ? 1.0 : -1.0;
-                    double lead = sgn * P.g[0], slope = fabs(P.g[1]);
-                    int64_t b = bmax;
-                    if (slope > 0.0 && lead > 0.0) {
-                        double est = lead / slope;
-                        if (est < (double)b) b = est < 2.0 ? 2 : (int64_t)est;
+                    double guess = poly_root_guess(P, sgn, (double)bmax);
+                    int64_t good = 0, bad = bmax + 1;
+                    int64_t b = (int64_t)(guess * 0.999);
+                    b = b < 2 ? 2 : (b > bmax ? bmax : b);
+                    for (int it = 0; it < 12 && bad - good > 1 + good / 64; it++) {
+                        if (poly_sign_definite(P, (double)b, sgn)) good = b;
+                        else bad = b;
+                        if (bad > bmax) b = good * 2 > bmax ? bmax : good * 2;  // gallop
+                        else b = good + (bad - good) / 2;
+                        if (b <= good || b >= bad) break;
                     }
-                    bool jumped = false;
-                    while (b >= 2) {
-                        double tl = lin_at(Lt, t, b - 1);  // t before the last step of the block
-                        if (!(tl > end || tl < start) && poly_sign_definite(P, (double)b, sgn)) {
-                            t = lin_at(Lt, t, b);
-                            px = lin_at(Lx, px, b);
-                            py = lin_at(Ly, py, b);
-                            pz = lin_at(Lz, pz, b);
-                            r = heart_f(px, py, pz);
-                            if (STATS) st->blocks++;
-                            jumped = true;
-                            break;
-                        }
-                        b >>= 1;
+                    if (good >= 2) {
+                        t = advance(t, s, good);
+                        px = advance(px, cx, good);
+                        py = advance(py, cy, good);
+                        pz = advance(pz, cz, good);
+                        r = heart_f(px, py, pz);
+                        if (STATS) st->blocks++;
+                        continue;
                     }
-                    if (jumped) continue;
                 }
             }
             // ---- one literal step (ray_marching.rs:38-51)

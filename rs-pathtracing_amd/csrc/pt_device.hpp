@@ -171,7 +171,7 @@ struct Scene {
     const int32_t *__restrict__ lin;
     const int32_t *__restrict__ march;
     const DBox *__restrict__ boxes;
-    int nnodes, nlin, nmarch, pad;
+    int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
 };
 
 // Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
@@ -189,10 +189,12 @@ PT_HD bool slab(const double *lo, const double *hi, const Ray &r, V3 inv, double
 // a candidate replaces the best one if it is nearer, or equally near and later
 // in the shape list — the linear scan's "later shape wins a tie" rule, which
 // makes the visiting order (uniform list, BVH, marched shapes last) irrelevant.
+// This part covers the uniform list and the BVH; marched shapes follow.
 template <bool STATS = false>
-PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, double *best_t, Ctr *ct = nullptr) {
-    double best = max_t;
-    int who = -1;
+PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
+                           Ctr *ct = nullptr) {
+    double best = *best_t;
+    int who = *who_out;
     // wave-uniform list (few JSON shapes): scalar loads of each shape
     for (int k = 0; k < sc.nlin; k++) {
         int i = sc.lin[k];
@@ -202,7 +204,6 @@ PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, dou
             who = i;
         }
     }
-    V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
     // threaded BVH over the remaining non-marched shapes
     int n = 0;
     while (n < sc.nnodes) {
@@ -222,8 +223,18 @@ PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, dou
             n = nd.skip;
         }
     }
+    *best_t = best;
+    *who_out = who;
+}
+
+template <bool STATS = false>
+PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, double *best_t, Ctr *ct = nullptr) {
+    double best = max_t;
+    int who = -1;
+    V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    closest_nomarch<STATS>(sc, r, inv, min_t, &best, &who, ct);
     // ray-marched shapes last, only if their padded box is entered before `best`
-    for (int k = 0; k < sc.nmarch; k++) {
+    for (int k = 0; k < ((sc.diag & 1) ? 0 : sc.nmarch); k++) {
         int i = sc.march[k];
         const DBox &b = sc.boxes[i];
         if (STATS) ct->c[C_MARCH_SLABS]++;
@@ -332,12 +343,10 @@ struct IdStack {
 
 // One bounce of ray_color (src/renderer/mod.rs:23-45).  Returns true when the
 // path ends, with the leaf radiance in *leaf; otherwise advances ray/depth.
+// Everything in a bounce after the closest hit (who, t) is known.
 template <int NW, bool STATS = false>
-PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng, double s11, V3 *leaf,
-                  Ctr *ct = nullptr) {
-    double t;
-    if (STATS) ct->c[C_BOUNCES]++;
-    int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
+PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng,
+                 double s11, V3 *leaf, Ctr *ct = nullptr) {
     if (who < 0) {
         *leaf = background(ray.d);
         return true;
@@ -387,6 +396,15 @@ PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, 
 }
 
 template <int NW, bool STATS = false>
+PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng, double s11, V3 *leaf,
+                  Ctr *ct = nullptr) {
+    double t;
+    if (STATS) ct->c[C_BOUNCES]++;
+    int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
+    return shade<NW, STATS>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
+}
+
+template <int NW, bool STATS = false>
 PT_HD V3 unwind(const Scene &sc, IdStack<NW> &stk, V3 c, Ctr *ct = nullptr) {
     while (stk.n > 0) {
         if (STATS) ct->c[C_UNWIND]++;
@@ -423,9 +441,18 @@ PT_HD Ray camera_ray(const FrameParams &P, uint32_t x, uint32_t y, Rng &rng) {
 }
 
 // trace_pixel_samples (renderer/mod.rs:151-155): in-order sum, then / spp.
-// One flat loop over bounces of all the pixel's samples: a lane whose path
-// ends starts its next sample at once instead of idling until every lane of
-// the wave has finished the current one.
+//
+// Each lane runs its pixel's samples as a small state machine, one pass of the
+// loop at a time:  TRACE (uniform list + BVH) -> SELECT (next marched shape
+// whose box is entered before the best hit; start its march) -> MARCH (a few
+// march iterations per pass) -> SHADE (hit point, scatter or leaf radiance;
+// next bounce or next sample).  A lane that is marching the Heart no longer
+// holds its whole wave: the other lanes keep tracing their own paths in the
+// same passes.  The per-lane sequence of operations, and so every value, is
+// the reference's.
+constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
+enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
+
 template <int NW, bool STATS = false>
 PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
@@ -436,16 +463,70 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
     uint32_t depth = P.depth;
     IdStack<NW> stk;
     stk.clear();
+    const int nmarch = (sc.diag & 1) ? 0 : sc.nmarch;
+    int phase = PH_TRACE, who = -1, km = 0, mshape = -1;
+    double best = 0.0;
+    V3 inv = v3(0.0, 0.0, 0.0);
+    march::MarchState ms;
+    march::MarchStats mst{0, 0, 0};
     for (;;) {
-        V3 leaf;
-        if (bounce<NW, STATS>(sc, ray, depth, stk, rng, P.s11, &leaf, ct)) {
-            acc = add(acc, unwind<NW, STATS>(sc, stk, leaf, ct));
-            if (STATS) ct->c[C_SAMPLES]++;
-            if (++s == P.spp) break;
-            rng.s = sample_key(P.seed, pixel, s);
-            ray = camera_ray(P, x, y, rng);
-            depth = P.depth;
+        if (phase == PH_TRACE) {
+            if (STATS) ct->c[C_BOUNCES]++;
+            inv = v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+            best = __builtin_inf();
+            who = -1;
+            closest_nomarch<STATS>(sc, ray, inv, T_MIN, &best, &who, ct);
+            km = 0;
+            phase = PH_SELECT;
         }
+        if (phase == PH_MARCH) {
+            for (int it = 0; it < MARCH_ITERS; it++) {
+                int st = march::march_iter<STATS>(ms, &mst);
+                if (st != march::M_RUNNING) {
+                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
+                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
+                        best = ms.t;
+                        who = mshape;
+                    }
+                    phase = PH_SELECT;
+                    break;
+                }
+            }
+        }
+        if (phase == PH_SELECT) {
+            phase = PH_SHADE;
+            while (km < nmarch) {
+                int i = sc.march[km++];
+                const DBox &b = sc.boxes[i];
+                if (STATS) ct->c[C_MARCH_SLABS]++;
+                if (!slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
+                const DShape &S = sc.shapes[i];
+                if (STATS) ct->c[C_TEST_MARCH]++;
+                V3 o = xf_point(S.inv, ray.o), d = xf_vector(S.inv, ray.d);
+                if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                    mshape = i;
+                    phase = PH_MARCH;
+                    break;
+                }
+            }
+        }
+        if (phase == PH_SHADE) {
+            V3 leaf;
+            if (shade<NW, STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct)) {
+                acc = add(acc, unwind<NW, STATS>(sc, stk, leaf, ct));
+                if (STATS) ct->c[C_SAMPLES]++;
+                if (++s == P.spp) break;
+                rng.s = sample_key(P.seed, pixel, s);
+                ray = camera_ray(P, x, y, rng);
+                depth = P.depth;
+            }
+            phase = PH_TRACE;
+        }
+    }
+    if (STATS) {
+        ct->c[C_MARCH_STEPS] += mst.steps;
+        ct->c[C_MARCH_BLOCKS] += mst.blocks;
+        ct->c[C_MARCH_TRIES] += mst.tries;
     }
     return divs(acc, (double)P.spp);
 }

@@ -140,7 +140,11 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.nnodes = s.nnodes;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
-    d.pad = 0;
+    static int diag = [] {
+        const char *e = getenv("PT_DIAG");
+        return e ? atoi(e) : 0;
+    }();
+    d.diag = diag;
     return d;
 }
 

@@ -276,75 +276,121 @@ struct MarchStats {
     uint32_t steps, blocks, tries;
 };
 
+// Resumable form of RayMarchingShape::ray_intersect (ray_marching.rs:20-74) so
+// a lane can march a few iterations per pass of the kernel's main loop while
+// the other lanes of its wave keep tracing.
+struct MarchState {
+    double t, px, py, pz, r, s, start, end, dx, dy, dz;
+    int pass, passes;
+};
+enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2 };
+
+// Bound test and start of the march; false if the ray misses the bound.
+PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
+                       MarchState *m) {
+    double start, end;
+    if (!heart_bound(ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+    m->start = start;
+    m->end = end;
+    m->s = step0;
+    m->t = start;
+    m->px = ox + dx * start;
+    m->py = oy + dy * start;
+    m->pz = oz + dz * start;
+    m->r = heart_f(m->px, m->py, m->pz);
+    m->dx = dx;
+    m->dy = dy;
+    m->dz = dz;
+    m->pass = 0;
+    m->passes = passes;
+    return true;
+}
+
+// One iteration of the march loop: a proven jump, or one literal step (after a
+// failed proof).  M_DONE: the passes ended (the caller applies the final
+// t-in-[min_t, max_t] test); M_MISS: t left [start, end].
+template <bool STATS>
+PT_HD int march_iter(MarchState &m, MarchStats *st) {
+    if (m.pass >= m.passes) return M_DONE;
+    if (m.t > m.end || m.t < m.start) return M_MISS;
+    double s = m.s;
+    double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
+    // ---- try to jump a block of b steps (exact advance + sign proof)
+    if (m.r != 0.0) {
+        int64_t bmax = steps_in_range(m.t, s, m.start, m.end, (int64_t)1 << 24);
+        if (bmax >= 2) {
+            Poly P;
+            heart_poly(m.px, m.py, m.pz, cx, cy, cz, &P);
+            if (STATS) st->tries++;
+            // largest provable block: start at the predicted crossing, drop by
+            // 4x until proven, then refine upward (gallop / bisect)
+            double sgn = m.r > 0.0 ? 1.0 : -1.0;
+            double guess = poly_root_guess(P, sgn, (double)bmax);
+            int64_t good = 0, bad = bmax + 1;
+            int64_t b = (int64_t)(guess * 0.999);
+            b = b < 2 ? 2 : (b > bmax ? bmax : b);
+            int evals = 0;
+            while (b >= 2 && evals < 10) {
+                evals++;
+                if (poly_sign_definite(P, (double)b, sgn)) {
+                    good = b;
+                    break;
+                }
+                bad = b;
+                b >>= 2;
+            }
+            while (good >= 2 && evals < 10 && bad - good > 1 + good / 16) {
+                b = bad > bmax ? (2 * good > bmax ? bmax : 2 * good) : good + (bad - good) / 2;
+                if (b <= good || b >= bad) break;
+                evals++;
+                if (poly_sign_definite(P, (double)b, sgn)) good = b;
+                else bad = b;
+            }
+            if (good >= 2) {
+                m.t = advance(m.t, s, good);
+                m.px = advance(m.px, cx, good);
+                m.py = advance(m.py, cy, good);
+                m.pz = advance(m.pz, cz, good);
+                m.r = heart_f(m.px, m.py, m.pz);
+                if (STATS) st->blocks++;
+                return M_RUNNING;
+            }
+        }
+    }
+    // ---- one literal step (ray_marching.rs:37-51)
+    m.t += s;
+    m.px += cx;
+    m.py += cy;
+    m.pz += cz;
+    double next = heart_f(m.px, m.py, m.pz);
+    if (STATS) st->steps++;
+    if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
+        m.pass = m.passes;
+        return M_DONE;
+    }
+    if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
+        m.s = s * -0.01;
+        m.r = next;
+        m.pass++;
+        return m.pass >= m.passes ? M_DONE : M_RUNNING;
+    }
+    m.r = next;
+    return M_RUNNING;
+}
+
 // RayMarchingShape::ray_intersect for the Heart in object space (o, d):
 // returns true with *t_out on a hit in [min_t, max_t].
 template <bool STATS>
 PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
                        double min_t, double max_t, double *t_out, MarchStats *st) {
-    double start, end;
-    if (!heart_bound(ox, oy, oz, dx, dy, dz, &start, &end)) return false;
-    double s = step0;
-    double t = start;
-    double px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-    double r = heart_f(px, py, pz);
-    bool hit = false;
-    for (int pass = 0; pass < passes && !hit; pass++) {
-        double cx = dx * s, cy = dy * s, cz = dz * s;
-        for (;;) {
-            if (t > end || t < start) return false;
-            // ---- try to jump a block of b steps (exact advance + sign proof)
-            if (r != 0.0) {
-                int64_t bmax = steps_in_range(t, s, start, end, (int64_t)1 << 24);
-                if (bmax >= 2) {
-                    Poly P;
-                    heart_poly(px, py, pz, cx, cy, cz, &P);
-                    if (STATS) st->tries++;
-                    // largest provable block: start at the predicted crossing,
-                    // gallop up while proven, then bisect between proven / not
-                    double sgn = r > 0.0 ? 1.0 : -1.0;
-                    double guess = poly_root_guess(P, sgn, (double)bmax);
-                    int64_t good = 0, bad = bmax + 1;
-                    int64_t b = (int64_t)(guess * 0.999);
-                    b = b < 2 ? 2 : (b > bmax ? bmax : b);
-                    for (int it = 0; it < 12 && bad - good > 1 + good / 64; it++) {
-                        if (poly_sign_definite(P, (double)b, sgn)) good = b;
-                        else bad = b;
-                        if (bad > bmax) b = good * 2 > bmax ? bmax : good * 2;  // gallop
-                        else b = good + (bad - good) / 2;
-                        if (b <= good || b >= bad) break;
-                    }
-                    if (good >= 2) {
-                        t = advance(t, s, good);
-                        px = advance(px, cx, good);
-                        py = advance(py, cy, good);
-                        pz = advance(pz, cz, good);
-                        r = heart_f(px, py, pz);
-                        if (STATS) st->blocks++;
-                        continue;
-                    }
-                }
-            }
-            // ---- one literal step (ray_marching.rs:38-51)
-            t += s;
-            px += cx;
-            py += cy;
-            pz += cz;
-            double next = heart_f(px, py, pz);
-            if (STATS) st->steps++;
-            if (fabs(next - 0.0) < 1e-15) {
-                hit = true;
-                break;
-            }
-            if ((r < 0.0 && next > 0.0) || (r > 0.0 && next < 0.0)) {
-                s *= -0.01;
-                r = next;
-                break;
-            }
-            r = next;
-        }
+    MarchState m;
+    if (!march_begin(step0, passes, ox, oy, oz, dx, dy, dz, &m)) return false;
+    int status;
+    while ((status = march_iter<STATS>(m, st)) == M_RUNNING) {
     }
-    if (t < min_t || t > max_t) return false;
-    *t_out = t;
+    if (status == M_MISS) return false;
+    if (m.t < min_t || m.t > max_t) return false;  // ray_marching.rs:55-57
+    *t_out = m.t;
     return true;
 }
 

@@ -159,6 +159,14 @@ int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint3
                   uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
                   uint64_t *counters);
 
+/* Diagnostic: render the whole frame (depth <= 8) with a timing build of the
+ * megakernel and return wave-level s_memtime cycles summed over waves per
+ * phase of its per-lane loop and pass counts: out[10] = {trace, march, select,
+ * shade cycles, lane passes (sum), lane march passes (sum), max lane passes,
+ * then shade split into: hit finish + material fetch, scatter, unwind/restart}. */
+int pt_profile_phases(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                      uint32_t samples_number, uint64_t seed, uint64_t *out);
+
 /* Display encode (src/bin/main.rs:281-289): sqrt -> clamp [0, 0.999] -> *256
  * -> u8, alpha 255; rgba is w*h*4 bytes. Host-side. */
 int pt_encode_rgba8(const double *rgb, size_t npix, uint8_t *rgba);

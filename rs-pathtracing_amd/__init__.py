@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
     "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
     "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_count_work", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -131,6 +131,7 @@ def lib():
                                              C.POINTER(u32), sz, d]),
         "pt_count_work": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u32), sz,
                                     C.POINTER(u64)]),
+        "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
         "pt_sample_key": (u64, [u64, u64, u64]),
         "pt_last_error": (C.c_char_p, []),
@@ -335,6 +336,17 @@ def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams,
                                int(samples_number), s, pixels.ctypes.data_as(C.POINTER(C.c_uint32)), len(pixels),
                                out))
     return dict(zip(COUNTERS, list(out)))
+
+
+def profile_phases(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,
+                   seed=None) -> dict:
+    """Wave-level phase timing of the megakernel's per-lane loop (pt_profile_phases)."""
+    out = (C.c_uint64 * 10)()
+    s = renderer.seed if seed is None else int(seed)
+    _check(lib().pt_profile_phases(renderer._h, C.byref(camera._c), img_params.width, img_params.height,
+                                   int(samples_number), s, out))
+    return dict(zip(["trace", "march", "select", "shade", "passes", "march_passes", "max_passes",
+                    "shade_finish", "shade_scatter", "shade_restart"], list(out)))
 
 
 def shard_tiles(width: int, height: int, rank: int, world: int) -> int:

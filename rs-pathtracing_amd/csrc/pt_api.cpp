@@ -62,6 +62,7 @@ struct pt_renderer {
     uint32_t depth = 0;
     hipStream_t stream = nullptr;
     DeviceScene ds;
+    WaveWorkspace ws;  // wavefront engine state (scenes with ray-marched shapes)
     double s11 = 0;
 
     // frame in flight
@@ -80,7 +81,7 @@ struct pt_renderer {
 extern "C" {
 
 const char *pt_last_error(void) { return g_err.c_str(); }
-const char *pt_version(void) { return "rs-pathtracing-amd 0.1.0 (gfx950, f64 megakernel)"; }
+const char *pt_version(void) { return "rs-pathtracing-amd 0.2.0 (gfx950, f64 megakernel + wavefront march engine)"; }
 
 uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample) { return sample_key(seed, pixel, sample); }
 
@@ -228,6 +229,8 @@ void pt_renderer_destroy(pt_renderer *r) {
     if (r->ds.lin) (void)hipFree(r->ds.lin);
     if (r->ds.march) (void)hipFree(r->ds.march);
     if (r->ds.boxes) (void)hipFree(r->ds.boxes);
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    wave_workspace_free(&r->ws);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -272,7 +275,7 @@ int pt_render_start(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h
         uint32_t t1 = t0 + band < ty ? t0 + band : ty;
         P.tile_begin = t0 * P.tiles_x;
         P.tile_count = (t1 - t0) * P.tiles_x;
-        HIP_TRY(launch_render(r->ds, P, r->d_frame, r->stream));
+        HIP_TRY(launch_render(r->ds, P, r->d_frame, r->stream, &r->ws));
         pt_renderer::Band b;
         b.row0 = t0 * TILE;
         b.row1 = t1 * TILE < h ? t1 * TILE : h;
@@ -346,7 +349,7 @@ int pt_render_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t 
     P.tile_begin = 0;
     P.tile_count = pt_shard_tiles(w, h, rank, world);
     hipStream_t st = stream ? (hipStream_t)stream : r->stream;
-    HIP_TRY(launch_render(r->ds, P, d_out, st));
+    HIP_TRY(launch_render(r->ds, P, d_out, st, &r->ws));
     return PT_OK;
 }
 
@@ -427,6 +430,24 @@ int pt_count_work(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, 
     HIP_TRY(launch_count_work(r->ds, P, dp.p, n, dc.p, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));
     HIP_TRY(hipMemcpy(counters, dc.p, C_COUNT * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_profile_phases(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
+                      uint64_t *out) {
+    if (!r || !cam || !out) return fail(PT_ERR_INVALID, "null argument");
+    if (r->depth > 8) return fail(PT_ERR_UNSUPPORTED, "phase profiling supports depth <= 8");
+    HIP_TRY(hipSetDevice(r->device));
+    FrameParams P = frame_params(r, *cam, w, h, spp, seed);
+    P.tile_count = pt_shard_tiles(w, h, 0, 1);
+    DevBuf<double> frame;
+    DevBuf<unsigned long long> acc;
+    HIP_TRY(frame.alloc((size_t)w * h * 3));
+    HIP_TRY(acc.alloc(10));
+    HIP_TRY(hipMemsetAsync(acc.p, 0, 10 * sizeof(unsigned long long), r->stream));
+    HIP_TRY(launch_render_timed(r->ds, P, frame.p, acc.p, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(hipMemcpy(out, acc.p, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 

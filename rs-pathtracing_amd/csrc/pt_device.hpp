@@ -172,6 +172,7 @@ struct Scene {
     const int32_t *__restrict__ march;
     const DBox *__restrict__ boxes;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
+    int march_trigger, march_keep;   // wave scheduling of the march block (trace_pixel)
 };
 
 // Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
@@ -283,6 +284,16 @@ PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
     return h;
 }
 
+// Diagnostic phase timing (TIMING build only): wave-level s_memtime deltas.
+struct PhaseTimes {
+    uint64_t trace, march, select, shade, passes, march_passes, finish, scatter, restart;
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_STAMP() __builtin_amdgcn_s_memtime()
+#else
+#define PT_STAMP() 0ull
+#endif
+
 // ------------------------------------------------------------ materials
 // random_in_unit_sphere (algebra/mod.rs:77-84): rejection in [-1, 1]^3
 template <bool STATS = false>
@@ -346,7 +357,7 @@ struct IdStack {
 // Everything in a bounce after the closest hit (who, t) is known.
 template <int NW, bool STATS = false>
 PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng,
-                 double s11, V3 *leaf, Ctr *ct = nullptr) {
+                 double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
         *leaf = background(ray.d);
         return true;
@@ -359,6 +370,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     if (STATS) ct->c[C_HITS]++;
     Hit h = finish(s, ray, t);
     const DMaterial &m = sc.mats[s.material];
+    if (tfin) *tfin = PT_STAMP();
     V3 dir;
     if (m.type == LAMBERTIAN) {  // material.rs:41-54
         if (STATS) ct->c[C_LAMBERT]++;
@@ -450,11 +462,23 @@ PT_HD Ray camera_ray(const FrameParams &P, uint32_t x, uint32_t y, Rng &rng) {
 // holds its whole wave: the other lanes keep tracing their own paths in the
 // same passes.  The per-lane sequence of operations, and so every value, is
 // the reference's.
-constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
+constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop (minimum)
+
+// Wave-level vote helpers (a host build is one lane).
+PT_HD uint64_t wave_ballot(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(p);
+#else
+    return p ? 1ull : 0ull;
+#endif
+}
+PT_HD int popc64(uint64_t m) { return __builtin_popcountll(m); }
 enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
 
-template <int NW, bool STATS = false>
-PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr) {
+
+template <int NW, bool STATS = false, bool TIMING = false>
+PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr,
+                     PhaseTimes *pt = nullptr) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
     V3 acc = v3(0.0, 0.0, 0.0);
     uint32_t s = 0;
@@ -469,7 +493,12 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
     V3 inv = v3(0.0, 0.0, 0.0);
     march::MarchState ms;
     march::MarchStats mst{0, 0, 0};
+    uint64_t ts = 0;
     for (;;) {
+        if (TIMING) {
+            ts = PT_STAMP();
+            pt->passes++;
+        }
         if (phase == PH_TRACE) {
             if (STATS) ct->c[C_BOUNCES]++;
             inv = v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
@@ -479,8 +508,19 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
             km = 0;
             phase = PH_SELECT;
         }
-        if (phase == PH_MARCH) {
-            for (int it = 0; it < MARCH_ITERS; it++) {
+        if (TIMING) {
+            uint64_t n = PT_STAMP();
+            pt->trace += n - ts;
+            ts = n;
+        }
+        // Lanes waiting to march are batched: the wave runs the march block
+        // only when >= march_trigger lanes wait (or every live lane does), and
+        // keeps iterating while >= march_keep lanes are still marching.
+        const uint64_t wm = wave_ballot(phase == PH_MARCH);
+        if (wm != 0 && (popc64(wm) >= sc.march_trigger || wm == wave_ballot(true)) && phase == PH_MARCH) {
+            if (TIMING) pt->march_passes++;
+            const int keep = wm == wave_ballot(true) ? (popc64(wm) + 1) / 2 : sc.march_keep;
+            for (int it = 0;; it++) {
                 int st = march::march_iter<STATS>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -491,7 +531,13 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                     phase = PH_SELECT;
                     break;
                 }
+                if (it + 1 >= MARCH_ITERS && popc64(wave_ballot(true)) < keep) break;
             }
+        }
+        if (TIMING) {
+            uint64_t n = PT_STAMP();
+            pt->march += n - ts;
+            ts = n;
         }
         if (phase == PH_SELECT) {
             phase = PH_SHADE;
@@ -510,9 +556,25 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                 }
             }
         }
+        if (TIMING) {
+            uint64_t n = PT_STAMP();
+            pt->select += n - ts;
+            ts = n;
+        }
         if (phase == PH_SHADE) {
             V3 leaf;
-            if (shade<NW, STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct)) {
+            uint64_t tf = 0;
+            const bool ended = shade<NW, STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
+                                                TIMING ? &tf : nullptr);
+            if (TIMING) {
+                uint64_t n = PT_STAMP();
+                if (tf) {
+                    pt->finish += tf - ts;
+                    pt->scatter += n - tf;
+                }
+                ts = n;
+            }
+            if (ended) {
                 acc = add(acc, unwind<NW, STATS>(sc, stk, leaf, ct));
                 if (STATS) ct->c[C_SAMPLES]++;
                 if (++s == P.spp) break;
@@ -522,7 +584,9 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
             }
             phase = PH_TRACE;
         }
+        if (TIMING) pt->restart += PT_STAMP() - ts;
     }
+    if (TIMING) pt->restart += PT_STAMP() - ts;
     if (STATS) {
         ct->c[C_MARCH_STEPS] += mst.steps;
         ct->c[C_MARCH_BLOCKS] += mst.blocks;

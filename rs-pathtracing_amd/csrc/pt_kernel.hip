@@ -127,7 +127,55 @@ __global__ __launch_bounds__(256) void count_work(dev::Scene sc, FrameParams P, 
         if (c.c[k]) atomicAdd(&ctr[k], (unsigned long long)c.c[k]);
 }
 
+// Diagnostic build: render_tiles with wave-level phase timing; lane 0 of each
+// wave adds its wave's stamps (the same for every lane: s_memtime is scalar).
+__global__ __launch_bounds__(256, 2) void render_tiles_timed(dev::Scene sc, FrameParams P, double *__restrict__ out,
+                                                             unsigned long long *__restrict__ acc) {
+    const uint32_t ti = P.tile_begin + blockIdx.x;
+    const uint32_t k = P.rank + ti * P.world;
+    const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint32_t lx = ((w & 1u) << 3) | (l & 7u), ly = ((w >> 1) << 3) | (l >> 3);
+    const uint32_t x = tx * TILE + lx, y = ty * TILE + ly;
+    dev::PhaseTimes pt = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    V3 c = dev::v3(0.0, 0.0, 0.0);
+    if (x < P.width && y < P.height) c = dev::trace_pixel<4, false, true>(sc, P, x, y, nullptr, &pt);
+    if (P.compact == 0 && x < P.width && y < P.height) {
+        double *dst = out + ((size_t)y * P.width + x) * 3;
+        dst[0] = c.x;
+        dst[1] = c.y;
+        dst[2] = c.z;
+    }
+    // per-lane pass counts: sum and max; wave-level times from the lane that
+    // kept the wave alive longest (largest stamp total; lowest such lane)
+    unsigned long long tot = pt.trace + pt.march + pt.select + pt.finish + pt.scatter + pt.restart, mx = tot;
+    for (int o = 32; o > 0; o >>= 1) {
+        unsigned long long v = __shfl_xor(mx, o, 64);
+        mx = v > mx ? v : mx;
+    }
+    const unsigned long long bal = __ballot(tot == mx);
+    if (l == (uint32_t)__ffsll((long long)bal) - 1) {
+        atomicAdd(&acc[0], (unsigned long long)pt.trace);
+        atomicAdd(&acc[1], (unsigned long long)pt.march);
+        atomicAdd(&acc[2], (unsigned long long)pt.select);
+        atomicAdd(&acc[3], (unsigned long long)(pt.finish + pt.scatter + pt.restart));
+        atomicAdd(&acc[7], (unsigned long long)pt.finish);
+        atomicAdd(&acc[8], (unsigned long long)pt.scatter);
+        atomicAdd(&acc[9], (unsigned long long)pt.restart);
+    }
+    atomicAdd(&acc[4], (unsigned long long)pt.passes);
+    atomicAdd(&acc[5], (unsigned long long)pt.march_passes);
+    atomicMax(&acc[6], (unsigned long long)pt.passes);
+}
+
 // ------------------------------------------------------------- launchers
+#ifndef PT_MARCH_TRIGGER_DEFAULT
+#define PT_MARCH_TRIGGER_DEFAULT 16
+#endif
+#ifndef PT_MARCH_KEEP_DEFAULT
+#define PT_MARCH_KEEP_DEFAULT 8
+#endif
+
 static dev::Scene dscene(const DeviceScene &s) {
     dev::Scene d;
     d.shapes = s.shapes;
@@ -145,6 +193,17 @@ static dev::Scene dscene(const DeviceScene &s) {
         return e ? atoi(e) : 0;
     }();
     d.diag = diag;
+    // march batching (trace_pixel): PT_MARCH_TRIGGER / PT_MARCH_KEEP override
+    static int trig = [] {
+        const char *e = getenv("PT_MARCH_TRIGGER");
+        return e ? atoi(e) : PT_MARCH_TRIGGER_DEFAULT;
+    }();
+    static int keep = [] {
+        const char *e = getenv("PT_MARCH_KEEP");
+        return e ? atoi(e) : PT_MARCH_KEEP_DEFAULT;
+    }();
+    d.march_trigger = trig;
+    d.march_keep = keep;
     return d;
 }
 
@@ -178,8 +237,20 @@ static int render_waves() {
     return w;
 }
 
-hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st) {
+hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
+                              WaveWorkspace *ws);
+
+static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
+    const char *e = getenv("PT_ENGINE");
+    if (e && e[0] == 'm') return false;
+    if (e && e[0] == 'w') return ws != nullptr;
+    return ws != nullptr && s.nmarch > 0 && (dscene(s).diag & 1) == 0;
+}
+
+hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
+                         WaveWorkspace *ws) {
     if (P.tile_count == 0) return hipSuccess;
+    if (use_wavefront(s, ws)) return launch_render_wave(dscene(s), P, out, st, ws);
     if (P.depth <= 8) {
         switch (render_waves()) {
         case 2: render_tiles<4, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
@@ -231,6 +302,13 @@ hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const u
     if (!n) return hipSuccess;
     PT_DISPATCH_NW(P.depth, (count_work<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dscene(s), P, pixels, n,
                                                                                          ctr)));
+    return hipGetLastError();
+}
+
+hipError_t launch_render_timed(const DeviceScene &s, const FrameParams &P, double *out, unsigned long long *acc,
+                               hipStream_t st) {
+    if (P.tile_count == 0) return hipSuccess;
+    render_tiles_timed<<<P.tile_count, 256, 0, st>>>(dscene(s), P, out, acc);
     return hipGetLastError();
 }
 

@@ -16,7 +16,19 @@ struct DeviceScene {
     int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
 };
 
-hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st);
+// Device workspace of the wavefront engine (pt_wave.hip), grown on demand and
+// reused by every frame of a renderer.
+struct WaveWorkspace {
+    void *base = nullptr;
+    size_t bytes = 0;
+};
+void wave_workspace_free(WaveWorkspace *ws);
+
+// Renders this rank's tiles of P into out.  Scenes with ray-marched shapes use
+// the wavefront engine (ws required), others the megakernel; PT_ENGINE=mega or
+// PT_ENGINE=wave in the environment forces one.
+hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
+                         WaveWorkspace *ws);
 hipError_t launch_unshard(const double *gathered, uint32_t width, uint32_t height, uint32_t world, double *frame,
                           hipStream_t st);
 hipError_t launch_closest_hit(const DeviceScene &s, const double *rays, size_t n, double min_t, double max_t,
@@ -28,5 +40,8 @@ hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const
 
 hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
                              unsigned long long *ctr, hipStream_t st);
+
+hipError_t launch_render_timed(const DeviceScene &s, const FrameParams &P, double *out, unsigned long long *acc,
+                               hipStream_t st);
 
 }  // namespace pt

@@ -1,0 +1,428 @@
+// pt_wave.hip — wavefront engine for scenes with ray-marched shapes.
+//
+// The megakernel (pt_kernel.hip) keeps a path in a lane for all of its
+// samples.  That is ideal while every lane does the same kind of work, but a
+// Heart march (tens of march iterations, ~1k VALU instructions each) runs for
+// a handful of lanes at a time and stalls the other 60 of its wave: on cornell
+// the megakernel spends >90 % of its wave time with few lanes active.
+//
+// Here the per-pixel sample loop (renderer/mod.rs:151-155, ray_color :23-45)
+// is cut at the closest hit into queue-connected kernels, one bounce per
+// launch (iteration `it`):
+//
+//   wf_bounce(it)  for every live path: shade the pending hit (material,
+//                  scatter, next ray — or end the path and store its sample
+//                  radiance), then trace the new ray through the uniform list
+//                  and the BVH.  A path whose ray enters a marched shape's
+//                  bound before its best hit goes to the march queue; the rest
+//                  go straight to the next live list.
+//   wf_march(it)   persistent lanes that refill themselves from the march
+//                  queue: every lane of every wave marches (select + march
+//                  iterations, pt_march.hpp) until the queue is drained, so
+//                  the march runs with full waves.
+//   wf_reduce      per pixel, adds the chunk's sample radiances in sample
+//                  order to the running sum (the reference's in-order sum),
+//                  and divides by spp after the last chunk.
+//
+// Path state lives in HBM, structure-of-arrays, one slot per (pixel, sample)
+// of a chunk: ~140 B per path for depth <= 8.  Queue pushes are wave-
+// aggregated (one atomic per wave), which keeps 8x8 pixel blocks together in
+// the lists.  Every value is computed by the same device functions, in the
+// same per-path order, as the megakernel and the oracle: the frame is
+// bit-identical.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "pt_device.hpp"
+#include "pt_kernel.hpp"
+
+namespace pt {
+
+using dev::Ray;
+using dev::V3;
+
+// Device view of the workspace for one chunk.
+struct WfView {
+    double *ox, *oy, *oz, *dx, *dy, *dz, *t;  // ray, best hit t
+    uint64_t *rng;
+    int32_t *who;    // best hit shape (-1: miss)
+    uint32_t *meta;  // depth | stack count << 8
+    uint64_t *stk;   // NW words per path, word k at stk[k * cap + id]
+    double *rx, *ry, *rz;  // sample radiance of finished paths
+    uint32_t *list[2], *mq;
+    uint32_t *cnt;  // per iteration: [0] live count, [1] march count, [2] march head, [3] unused
+    double *acc;    // running per-pixel sums (3 per pixel of the tile group)
+    uint32_t cap;   // path slots
+    uint32_t npix;  // pixels of the tile group (tiles * 256)
+    uint32_t s0, ns;  // sample range of the chunk
+    uint32_t tile0;   // first tile of the group (index in this rank's tile list)
+};
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Wave-aggregated queue push: every active lane calls it; lanes with p get
+// consecutive slots (in lane order) from one atomic.
+__device__ __forceinline__ uint32_t wave_push(uint32_t *counter, bool p) {
+    const uint64_t m = __ballot(p);
+    if (m == 0) return 0;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    return base + below;
+}
+
+// Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
+// thread-in-tile laid out as render_tiles' 4 waves of 8x8.
+__device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v, uint32_t id, uint32_t *x,
+                                           uint32_t *y, uint32_t *s_local, uint32_t *pix_local) {
+    const uint32_t within = id % v.npix;
+    *s_local = id / v.npix;
+    *pix_local = within;
+    const uint32_t ti = v.tile0 + within / (TILE * TILE);
+    const uint32_t th = within % (TILE * TILE);
+    const uint32_t k = P.rank + ti * P.world;
+    const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
+    const uint32_t w = th >> 6, l = th & 63;
+    *x = tx * TILE + (((w & 1u) << 3) | (l & 7u));
+    *y = ty * TILE + (((w >> 1) << 3) | (l >> 3));
+}
+
+// One bounce for every live path of iteration `it` (it == 0: camera rays).
+template <int NW, bool FIRST>
+__global__ __launch_bounds__(256) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it) {
+    const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
+    const uint32_t *lin_ = v.list[it & 1];
+    uint32_t *lout = v.list[(it + 1) & 1];
+    uint32_t *cnext = &v.cnt[(it + 1) * 4 + 0];
+    uint32_t *cmarch = &v.cnt[it * 4 + 1];
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
+        const uint32_t i = base + threadIdx.x;
+        bool live = i < count;
+        uint32_t id = 0;
+        Ray ray;
+        dev::Rng rng{0};
+        uint32_t depth = 0;
+        dev::IdStack<NW> stk;
+        stk.clear();
+        if (live) {
+            if (FIRST) {
+                id = i;
+                uint32_t x, y, sl, pl;
+                slot_pixel(P, v, id, &x, &y, &sl, &pl);
+                if (x >= P.width || y >= P.height || sl >= v.ns) {
+                    live = false;
+                } else {
+                    rng.s = dev::sample_key(P.seed, (uint64_t)x + (uint64_t)y * P.width, v.s0 + sl);
+                    ray = dev::camera_ray(P, x, y, rng);
+                    depth = P.depth;
+                }
+            } else {
+                id = lin_[i];
+                ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
+                ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
+                rng.s = v.rng[id];
+                const uint32_t meta = v.meta[id];
+                depth = meta & 0xffu;
+                stk.n = (int)(meta >> 8);
+#pragma unroll
+                for (int k = 0; k < NW; k++) stk.w[k] = v.stk[(size_t)k * v.cap + id];
+                V3 leaf;
+                if (dev::shade<NW>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                    const V3 c = dev::unwind<NW>(sc, stk, leaf);
+                    v.rx[id] = c.x;
+                    v.ry[id] = c.y;
+                    v.rz[id] = c.z;
+                    live = false;
+                }
+            }
+        }
+        bool need_march = false;
+        if (live) {
+            const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+            double best = __builtin_inf();
+            int who = -1;
+            dev::closest_nomarch(sc, ray, inv, T_MIN, &best, &who);
+            // does any marched shape's bound start before the best hit? (the
+            // march kernel repeats this select and marches)
+            for (int k = 0; k < sc.nmarch && !need_march; k++) {
+                const int s = sc.march[k];
+                const DBox &b = sc.boxes[s];
+                if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
+                const DShape &S = sc.shapes[s];
+                const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
+                double st, en;
+                need_march = march::heart_bound(o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
+            }
+            v.ox[id] = ray.o.x;
+            v.oy[id] = ray.o.y;
+            v.oz[id] = ray.o.z;
+            v.dx[id] = ray.d.x;
+            v.dy[id] = ray.d.y;
+            v.dz[id] = ray.d.z;
+            v.t[id] = best;
+            v.who[id] = who;
+            v.rng[id] = rng.s;
+            v.meta[id] = depth | ((uint32_t)stk.n << 8);
+#pragma unroll
+            for (int k = 0; k < NW; k++) v.stk[(size_t)k * v.cap + id] = stk.w[k];
+        }
+        const uint32_t qm = wave_push(cmarch, live && need_march);
+        if (live && need_march) v.mq[qm] = id;
+        const uint32_t qn = wave_push(cnext, live && !need_march);
+        if (live && !need_march) lout[qn] = id;
+    }
+}
+
+// Marches of iteration `it`: persistent lanes, each refilled from the queue as
+// soon as its job is done.  A job is the select loop over the marched shapes
+// (trace_pixel's SELECT/MARCH phases) for one path; its result (best, who)
+// goes back to the path, which joins the next live list.
+__global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it) {
+    const uint32_t count = v.cnt[it * 4 + 1];
+    uint32_t *head = &v.cnt[it * 4 + 2];
+    uint32_t *cnext = &v.cnt[(it + 1) * 4 + 0];
+    uint32_t *lout = v.list[(it + 1) & 1];
+    bool busy = false, retired = false, marching = false;
+    uint32_t id = 0;
+    int km = 0, who = -1, mshape = -1;
+    double best = 0.0;
+    Ray ray;
+    V3 inv = dev::v3(0.0, 0.0, 0.0);
+    march::MarchState ms;
+    march::MarchStats mst{0, 0, 0};
+    for (;;) {
+        // refill idle lanes with one atomic per wave
+        const bool want = !busy && !retired;
+        const uint64_t m = __ballot(want);
+        if (m != 0) {
+            const int leader = __ffsll((long long)m) - 1;
+            uint32_t base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(head, (uint32_t)__popcll(m));
+            base = __shfl(base, leader, 64);
+            if (want) {
+                const uint32_t q =
+                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (q < count) {
+                    id = v.mq[q];
+                    ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
+                    ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
+                    inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+                    best = v.t[id];
+                    who = v.who[id];
+                    km = 0;
+                    marching = false;
+                    busy = true;
+                } else {
+                    retired = true;
+                }
+            }
+        }
+        if (__ballot(busy) == 0) break;  // queue drained and no lane holds a job
+        bool done = false;
+        if (busy) {
+            if (marching) {
+                const int st = march::march_iter<false>(ms, &mst);
+                if (st != march::M_RUNNING) {
+                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
+                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
+                        best = ms.t;
+                        who = mshape;
+                    }
+                    marching = false;
+                }
+            } else {
+                // select: next marched shape whose bound is entered before `best`
+                while (km < sc.nmarch) {
+                    const int s = sc.march[km++];
+                    const DBox &b = sc.boxes[s];
+                    if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
+                    const DShape &S = sc.shapes[s];
+                    const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
+                    if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                        mshape = s;
+                        marching = true;
+                        break;
+                    }
+                }
+                if (!marching) {
+                    v.t[id] = best;
+                    v.who[id] = who;
+                    done = true;
+                }
+            }
+        }
+        const uint32_t qn = wave_push(cnext, done);
+        if (done) {
+            lout[qn] = id;
+            busy = false;
+        }
+    }
+}
+
+// In-order per-pixel sum of the chunk's samples; mean after the last chunk.
+__global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int first, int last,
+                                                 double *__restrict__ out) {
+    const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pl >= v.npix) return;
+    uint32_t x, y, sl, pl2;
+    slot_pixel(P, v, pl, &x, &y, &sl, &pl2);
+    const uint32_t ti = v.tile0 + pl / (TILE * TILE), th = pl % (TILE * TILE);
+    const uint32_t w = th >> 6, l = th & 63;
+    const uint32_t lx = ((w & 1u) << 3) | (l & 7u), ly = ((w >> 1) << 3) | (l >> 3);
+    double *dst = P.compact ? out + ((size_t)ti * (TILE * TILE) + ly * TILE + lx) * 3
+                            : out + ((size_t)y * P.width + x) * 3;
+    if (x >= P.width || y >= P.height) {
+        if (P.compact && last) dst[0] = dst[1] = dst[2] = 0.0;
+        return;
+    }
+    V3 a = first ? dev::v3(0.0, 0.0, 0.0) : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
+    for (uint32_t s = 0; s < v.ns; s++) {
+        const size_t id = (size_t)s * v.npix + pl;
+        a = dev::add(a, dev::v3(v.rx[id], v.ry[id], v.rz[id]));
+    }
+    if (last) {
+        const V3 c = dev::divs(a, (double)P.spp);
+        dst[0] = c.x;
+        dst[1] = c.y;
+        dst[2] = c.z;
+    } else {
+        v.acc[pl * 3 + 0] = a.x;
+        v.acc[pl * 3 + 1] = a.y;
+        v.acc[pl * 3 + 2] = a.z;
+    }
+}
+
+// ------------------------------------------------------------- host driver
+static size_t path_bytes(int nw) { return 7 * 8 + 8 + 4 + 4 + (size_t)nw * 8 + 3 * 8 + 3 * 4; }
+
+static uint32_t wf_cap_paths() {
+    const char *e = getenv("PT_WF_PATHS");
+    long v = e ? atol(e) : (1l << 24);
+    return (uint32_t)(v < 256 ? 256 : (v > (1l << 28) ? (1l << 28) : v));
+}
+
+void wave_workspace_free(WaveWorkspace *ws) {
+    if (ws->base) (void)hipFree(ws->base);
+    ws->base = nullptr;
+    ws->bytes = 0;
+}
+
+static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
+    if (bytes <= ws->bytes) return hipSuccess;
+    wave_workspace_free(ws);
+    hipError_t e = hipMalloc(&ws->base, bytes);
+    if (e != hipSuccess) {
+        ws->base = nullptr;
+        return e;
+    }
+    ws->bytes = bytes;
+    return hipSuccess;
+}
+
+template <int NW>
+static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
+                                 WaveWorkspace *ws) {
+    const uint32_t cap_want = wf_cap_paths();
+    // tile groups (only for frames beyond cap_want pixels), then sample chunks
+    const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
+    const uint32_t ntiles = P0.tile_count;
+    const uint32_t group_tiles = ntiles < tiles_per_group ? ntiles : tiles_per_group;
+    const uint32_t npix_max = group_tiles * TILE * TILE;
+    uint32_t ns = cap_want / npix_max;
+    if (ns < 1) ns = 1;
+    if (ns > P0.spp) ns = P0.spp;
+    const uint32_t cap = ns * npix_max;
+    const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
+    const size_t cnt_words = (size_t)(iters + 2) * 4;
+    const size_t bytes = (size_t)cap * path_bytes(NW) + (size_t)npix_max * 24 + cnt_words * 4 + 1024;
+    hipError_t e = reserve(ws, bytes);
+    if (e != hipSuccess) return e;
+    // carve the workspace
+    char *p = (char *)ws->base;
+    auto take = [&](size_t n) {
+        char *r = p;
+        p += (n + 255) & ~(size_t)255;
+        return (void *)r;
+    };
+    WfView v;
+    v.ox = (double *)take((size_t)cap * 8);
+    v.oy = (double *)take((size_t)cap * 8);
+    v.oz = (double *)take((size_t)cap * 8);
+    v.dx = (double *)take((size_t)cap * 8);
+    v.dy = (double *)take((size_t)cap * 8);
+    v.dz = (double *)take((size_t)cap * 8);
+    v.t = (double *)take((size_t)cap * 8);
+    v.rng = (uint64_t *)take((size_t)cap * 8);
+    v.who = (int32_t *)take((size_t)cap * 4);
+    v.meta = (uint32_t *)take((size_t)cap * 4);
+    v.stk = (uint64_t *)take((size_t)cap * 8 * NW);
+    v.rx = (double *)take((size_t)cap * 8);
+    v.ry = (double *)take((size_t)cap * 8);
+    v.rz = (double *)take((size_t)cap * 8);
+    v.list[0] = (uint32_t *)take((size_t)cap * 4);
+    v.list[1] = (uint32_t *)take((size_t)cap * 4);
+    v.mq = (uint32_t *)take((size_t)cap * 4);
+    v.acc = (double *)take((size_t)npix_max * 24);
+    v.cnt = (uint32_t *)take(cnt_words * 4);
+    if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
+
+    // persistent march grid: exactly the resident blocks of the device
+    static uint32_t march_blocks = [] {
+        int dev = 0, cus = 256, per = 3;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            hipDeviceProp_t pr;
+            if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
+        }
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march, 256, 0) == hipSuccess && occ > 0) per = occ;
+        return (uint32_t)(cus * per);
+    }();
+    for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
+        const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
+        v.tile0 = P0.tile_begin + g0;
+        v.npix = gt * TILE * TILE;
+        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns) {
+            v.s0 = s0;
+            v.ns = P0.spp - s0 < ns ? P0.spp - s0 : ns;
+            v.cap = cap;
+            const uint32_t paths = v.ns * v.npix;
+            e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, st);
+            if (e != hipSuccess) return e;
+            uint32_t bb = (paths + 255) / 256;
+            if (bb > 8192) bb = 8192;
+            // iteration 0: slots [0, paths) are the chunk's camera rays
+            wf_bounce<NW, true><<<(paths + 255) / 256, 256, 0, st>>>(sc, P0, v, 0);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            for (int it = 0; it < iters; it++) {
+                if (it > 0) {
+                    wf_bounce<NW, false><<<bb, 256, 0, st>>>(sc, P0, v, it);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                }
+                if (it < iters - 1) {
+                    wf_march<<<march_blocks, 256, 0, st>>>(sc, v, it);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                }
+            }
+            wf_reduce<<<(v.npix + 255) / 256, 256, 0, st>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
+                              WaveWorkspace *ws) {
+    if (P.tile_count == 0 || P.spp == 0) return hipSuccess;
+    if (P.depth <= 8) return render_wave_nw<4>(sc, P, out, st, ws);
+    if (P.depth <= 16) return render_wave_nw<8>(sc, P, out, st, ws);
+    if (P.depth <= 32) return render_wave_nw<16>(sc, P, out, st, ws);
+    return render_wave_nw<32>(sc, P, out, st, ws);
+}
+
+}  // namespace pt

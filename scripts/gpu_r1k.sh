@@ -1,0 +1,8 @@
+set -e
+mkdir -p gpurun_out/r1k
+cd /tmp && export TMPDIR=/tmp
+B="python3 $GRAFT_REPO_ROOT/bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r1k/a -o p --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU -- $B > $GRAFT_REPO_ROOT/gpurun_out/r1k/a.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r1k/b -o p --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAIT_INST_ANY -- $B > $GRAFT_REPO_ROOT/gpurun_out/r1k/b.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r1k/c -o p --pmc FETCH_SIZE -- $B > $GRAFT_REPO_ROOT/gpurun_out/r1k/c.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r1k/d -o p --pmc WRITE_SIZE -- $B > $GRAFT_REPO_ROOT/gpurun_out/r1k/d.log 2>&1

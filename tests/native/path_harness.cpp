@@ -39,6 +39,8 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.nlin = (int)b->acc.lin.size();
         b->view.nmarch = (int)b->acc.march.size();
         b->view.diag = 0;
+        b->view.march_trigger = 1;
+        b->view.march_keep = 1;
         b->s11 = uniform_incl_scale(-1.0, 1.0);
         return b;
     } catch (...) {

@@ -187,3 +187,80 @@ def test_count_work_diagnostic(pt, cornell):
     assert cnt["bounces"] >= cnt["samples"]
     assert cnt["test_rect"] >= 6 * cnt["bounces"]  # the 6 uniform rectangles are tested every bounce
     assert cnt["test_march"] > 0 and cnt["march_tries"] > 0
+
+
+class _env:
+    """Temporarily set engine knobs (read by the library at every launch)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        import os
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        import os
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_engines_agree_with_oracle(pt, cornell):
+    """Cornell has the ray-marched Heart, so the default engine is the
+    wavefront one; the megakernel must give the same bits, and both the
+    oracle's."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam, ip = ps.camera(), pt.ImageParams(80, 45)
+    wave = r.render(cam, ip, 3, seed=21)
+    with _env(PT_ENGINE="mega"):
+        mega = r.render(cam, ip, 3, seed=21)
+    assert np.array_equal(wave, mega)
+    check_image(wave, osc.render(80, 45, 3, 8, 21))
+
+
+def test_wavefront_chunks_and_tile_groups(pt, cornell):
+    """A tiny path budget forces one-tile groups and one-sample chunks: the
+    running per-pixel sums must still add samples in order."""
+    with _env(PT_WF_PATHS=300):
+        img, ref = render_pair(pt, cornell, 37, 21, 3, 8, seed=9)
+    check_image(img, ref)
+    with _env(PT_WF_PATHS=256 * 7):  # 7 tiles x 1 spp per chunk, ragged last group
+        img, ref = render_pair(pt, cornell, 70, 45, 2, 8, seed=10)
+    check_image(img, ref)
+
+
+def test_wavefront_deep_paths(pt, spheres, cornell):
+    """Depth 50 (the bins' depth) through the wavefront engine: 32-word stacks."""
+    with _env(PT_ENGINE="wave"):
+        img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
+        check_image(img, ref)
+        img, ref = render_pair(pt, cornell, 24, 16, 2, 20, seed=6)
+        check_image(img, ref)
+
+
+def test_wavefront_shards(pt, cornell):
+    """Compact per-rank shards from the wavefront engine un-interleave to the
+    single-rank frame."""
+    import torch
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h, spp, world = 53, 40, 2, 2
+    stream = torch.cuda.current_stream().cuda_stream
+    per = pt.shard_tiles(w, h, 0, world)
+    g = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    for rank in range(world):
+        r.render_device(cam, w, h, spp, 8, rank, world, g.data_ptr() + rank * per * 256 * 3 * 8, stream)
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # stream handle 0 is the renderer's own stream
+    pt.unshard_device(g.data_ptr(), w, h, world, frame.data_ptr(), stream)
+    torch.cuda.synchronize()
+    with _env(PT_ENGINE="mega"):
+        want = r.render(cam, pt.ImageParams(w, h), spp, seed=8)
+    assert np.array_equal(frame.cpu().numpy().reshape(-1, 3), want)

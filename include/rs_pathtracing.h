@@ -159,6 +159,13 @@ int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint3
                   uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
                   uint64_t *counters);
 
+/* The RayMarchingShape march alone (src/world/shapes/ray_marching.rs:20-74,
+ * Heart) on n object-space jobs of 8 doubles {step, passes, o[3], d[3], 0}:
+ * t_out = the march's final t, status = 1 if the passes ended (a hit before
+ * the caller's [min_t, max_t] test) else 0, iters = skipping-march iterations.
+ * Diagnostic / parity probe. */
+int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters);
+
 /* Diagnostic: render the whole frame (depth <= 8) with a timing build of the
  * megakernel and return wave-level s_memtime cycles summed over waves per
  * phase of its per-lane loop and pass counts: out[10] = {trace, march, select,

@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
     "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
     "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -131,6 +131,8 @@ def lib():
                                              C.POINTER(u32), sz, d]),
         "pt_count_work": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u32), sz,
                                     C.POINTER(u64)]),
+        "pt_march_jobs": (C.c_int, [vp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                    C.POINTER(C.c_uint32)]),
         "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
         "pt_sample_key": (u64, [u64, u64, u64]),
@@ -336,6 +338,21 @@ def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams,
                                int(samples_number), s, pixels.ctypes.data_as(C.POINTER(C.c_uint32)), len(pixels),
                                out))
     return dict(zip(COUNTERS, list(out)))
+
+
+def march_jobs(renderer: "HipRenderer", jobs):
+    """The skipping Heart march alone on the GPU (pt_march_jobs): jobs is an
+    (n, 8) float64 array {step, passes, o, d, 0}; returns (t, hit, iters)."""
+    import numpy as np
+    jobs = np.ascontiguousarray(jobs, dtype=np.float64).reshape(-1, 8)
+    n = len(jobs)
+    t = np.zeros(n)
+    st = np.zeros(n, np.int32)
+    it = np.zeros(n, np.uint32)
+    dp = C.POINTER(C.c_double)
+    _check(lib().pt_march_jobs(renderer._h, jobs.ctypes.data_as(dp), n, t.ctypes.data_as(dp),
+                               st.ctypes.data_as(C.POINTER(C.c_int32)), it.ctypes.data_as(C.POINTER(C.c_uint32))))
+    return t, st.astype(bool), it
 
 
 def profile_phases(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,

@@ -433,6 +433,26 @@ int pt_count_work(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, 
     return PT_OK;
 }
 
+int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters) {
+    if (!r || (n && (!jobs || !t_out || !status || !iters))) return fail(PT_ERR_INVALID, "null argument");
+    if (n == 0) return PT_OK;
+    HIP_TRY(hipSetDevice(r->device));
+    DevBuf<double> dj, dt;
+    DevBuf<int32_t> ds;
+    DevBuf<uint32_t> di;
+    HIP_TRY(dj.alloc(n * 8));
+    HIP_TRY(dt.alloc(n));
+    HIP_TRY(ds.alloc(n));
+    HIP_TRY(di.alloc(n));
+    HIP_TRY(hipMemcpyAsync(dj.p, jobs, n * 8 * sizeof(double), hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(launch_march_probe(dj.p, n, dt.p, ds.p, di.p, r->stream));
+    HIP_TRY(hipMemcpyAsync(t_out, dt.p, n * sizeof(double), hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipMemcpyAsync(status, ds.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipMemcpyAsync(iters, di.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    return PT_OK;
+}
+
 int pt_profile_phases(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
                       uint64_t *out) {
     if (!r || !cam || !out) return fail(PT_ERR_INVALID, "null argument");

@@ -172,7 +172,6 @@ struct Scene {
     const int32_t *__restrict__ march;
     const DBox *__restrict__ boxes;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
-    int march_trigger, march_keep;   // wave scheduling of the march block (trace_pixel)
 };
 
 // Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
@@ -462,17 +461,8 @@ PT_HD Ray camera_ray(const FrameParams &P, uint32_t x, uint32_t y, Rng &rng) {
 // holds its whole wave: the other lanes keep tracing their own paths in the
 // same passes.  The per-lane sequence of operations, and so every value, is
 // the reference's.
-constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop (minimum)
+constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
 
-// Wave-level vote helpers (a host build is one lane).
-PT_HD uint64_t wave_ballot(bool p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __ballot(p);
-#else
-    return p ? 1ull : 0ull;
-#endif
-}
-PT_HD int popc64(uint64_t m) { return __builtin_popcountll(m); }
 enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
 
 
@@ -513,14 +503,9 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
             pt->trace += n - ts;
             ts = n;
         }
-        // Lanes waiting to march are batched: the wave runs the march block
-        // only when >= march_trigger lanes wait (or every live lane does), and
-        // keeps iterating while >= march_keep lanes are still marching.
-        const uint64_t wm = wave_ballot(phase == PH_MARCH);
-        if (wm != 0 && (popc64(wm) >= sc.march_trigger || wm == wave_ballot(true)) && phase == PH_MARCH) {
+        if (phase == PH_MARCH) {
             if (TIMING) pt->march_passes++;
-            const int keep = wm == wave_ballot(true) ? (popc64(wm) + 1) / 2 : sc.march_keep;
-            for (int it = 0;; it++) {
+            for (int it = 0; it < MARCH_ITERS; it++) {
                 int st = march::march_iter<STATS>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -531,7 +516,6 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                     phase = PH_SELECT;
                     break;
                 }
-                if (it + 1 >= MARCH_ITERS && popc64(wave_ballot(true)) < keep) break;
             }
         }
         if (TIMING) {

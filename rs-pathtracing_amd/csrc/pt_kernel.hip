@@ -127,6 +127,26 @@ __global__ __launch_bounds__(256) void count_work(dev::Scene sc, FrameParams P, 
         if (c.c[k]) atomicAdd(&ctr[k], (unsigned long long)c.c[k]);
 }
 
+// The skipping march alone on explicit object-space jobs (8 doubles each:
+// step, passes, o[3], d[3], unused): t, status (1 hit / 0 miss) and iteration
+// count, for checking the device build of pt_march.hpp against the host's.
+__global__ __launch_bounds__(256) void march_probe(const double *__restrict__ jobs, size_t n, double *__restrict__ t_out,
+                                                   int32_t *__restrict__ status, uint32_t *__restrict__ iters) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double *j = jobs + i * 8;
+    march::MarchState m;
+    int st = march::M_MISS;
+    uint32_t k = 0;
+    if (march::march_begin(j[0], (int)j[1], j[2], j[3], j[4], j[5], j[6], j[7], &m)) {
+        march::MarchStats ms{0, 0, 0};
+        while ((st = march::march_iter<false>(m, &ms)) == march::M_RUNNING) k++;
+    }
+    t_out[i] = m.t;
+    status[i] = st == march::M_DONE ? 1 : 0;
+    iters[i] = k;
+}
+
 // Diagnostic build: render_tiles with wave-level phase timing; lane 0 of each
 // wave adds its wave's stamps (the same for every lane: s_memtime is scalar).
 __global__ __launch_bounds__(256, 2) void render_tiles_timed(dev::Scene sc, FrameParams P, double *__restrict__ out,
@@ -169,13 +189,6 @@ __global__ __launch_bounds__(256, 2) void render_tiles_timed(dev::Scene sc, Fram
 }
 
 // ------------------------------------------------------------- launchers
-#ifndef PT_MARCH_TRIGGER_DEFAULT
-#define PT_MARCH_TRIGGER_DEFAULT 16
-#endif
-#ifndef PT_MARCH_KEEP_DEFAULT
-#define PT_MARCH_KEEP_DEFAULT 8
-#endif
-
 static dev::Scene dscene(const DeviceScene &s) {
     dev::Scene d;
     d.shapes = s.shapes;
@@ -193,17 +206,6 @@ static dev::Scene dscene(const DeviceScene &s) {
         return e ? atoi(e) : 0;
     }();
     d.diag = diag;
-    // march batching (trace_pixel): PT_MARCH_TRIGGER / PT_MARCH_KEEP override
-    static int trig = [] {
-        const char *e = getenv("PT_MARCH_TRIGGER");
-        return e ? atoi(e) : PT_MARCH_TRIGGER_DEFAULT;
-    }();
-    static int keep = [] {
-        const char *e = getenv("PT_MARCH_KEEP");
-        return e ? atoi(e) : PT_MARCH_KEEP_DEFAULT;
-    }();
-    d.march_trigger = trig;
-    d.march_keep = keep;
     return d;
 }
 
@@ -302,6 +304,13 @@ hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const u
     if (!n) return hipSuccess;
     PT_DISPATCH_NW(P.depth, (count_work<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dscene(s), P, pixels, n,
                                                                                          ctr)));
+    return hipGetLastError();
+}
+
+hipError_t launch_march_probe(const double *jobs, size_t n, double *t, int32_t *status, uint32_t *iters,
+                              hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    march_probe<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(jobs, n, t, status, iters);
     return hipGetLastError();
 }
 

@@ -41,6 +41,8 @@ hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const
 hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
                              unsigned long long *ctr, hipStream_t st);
 
+hipError_t launch_march_probe(const double *jobs, size_t n, double *t, int32_t *status, uint32_t *iters,
+                              hipStream_t st);
 hipError_t launch_render_timed(const DeviceScene &s, const FrameParams &P, double *out, unsigned long long *acc,
                                hipStream_t st);
 

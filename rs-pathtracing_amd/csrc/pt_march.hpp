@@ -31,6 +31,14 @@
 #define PT_HD __host__ __device__ __forceinline__
 #endif
 
+// Host-only profiling hooks (tools/march_prof.cpp); no-ops in the product.
+#ifndef PT_MPROF
+#define PT_MPROF(field) ((void)0)
+#endif
+#ifndef PT_MCAPTURE
+#define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz) ((void)0)
+#endif
+
 namespace pt {
 namespace march {
 
@@ -71,61 +79,88 @@ PT_HD bool heart_bound(double ox, double oy, double oz, double dx, double dy, do
 }
 
 // ------------------------------------------------------- closed-form adds
+// All closed-form arithmetic is done in f64: grid integers (X, R, spans) stay
+// below 2^53, so every product and sum below is exact, and the GPU never
+// needs emulated int64 multiplies or divisions.
 struct Lin {
-    int64_t X = 0, R = 0;  // value = X * 2^sh, step = R * 2^sh
-    int sh = 0;            // e - 52
-    bool frozen = false;   // c == 0: fl(x + 0) = x forever
+    double X = 0.0, R = 0.0;  // value = X * u, step = R * u (X, R integers)
+    double u = 0.0;           // grid of x's binade, 2^(e-52)
+    bool frozen = false;      // c == 0: fl(x + 0) = x forever
 };
 
 constexpr int64_t BIG = (int64_t)1 << 40;
+constexpr double BIGD = 1099511627776.0;  // 2^40
 PT_HD int64_t imin(int64_t a, int64_t b) { return a < b ? a : b; }
+
+// 1/x to a few ulp: the hardware reciprocal (v_rcp_f64 is only good to about
+// 2^-23 relative) polished by two Newton steps; callers correct the floor of a
+// quotient computed with it by exact integer tests.  (Explicit fma here is not
+// a contraction of the reference's arithmetic: the result is only an estimate.)
+PT_HD double approx_rcp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+#else
+    return 1.0 / x;
+#endif
+}
+
+// floor(n / d) for integers 0 <= n, 1 <= d, n / d < 2^41, all exact in f64.
+PT_HD double floor_div(double n, double d) {
+    double k = floor(n * approx_rcp(d));
+    // the estimate is within a fraction of 1 of n / d; two exact corrections
+    if (k * d > n) k -= 1.0;
+    if (k * d > n) k -= 1.0;
+    if ((k + 1.0) * d <= n) k += 1.0;
+    if ((k + 1.0) * d <= n) k += 1.0;
+    return k;
+}
 
 // Largest B such that the first B additions fl(x_j + c), j = 0..B-1, are all
 // x_j + R*u exactly; 0 if the closed form does not apply here.
 PT_HD int64_t lin_init(double x, double c, Lin *L) {
+    PT_MPROF(lin_init);
     L->frozen = false;
     if (c == 0.0) {
         L->frozen = true;
         return BIG;
     }
-    if (!(x != 0.0) || !(fabs(x) < 1e300) || !(fabs(c) < 1e300)) return 0;  // zero, inf, NaN
-    int e = ilogb(x);
+    if (!(x != 0.0) || !(fabs(x) < 1e300) || !(fabs(c) < 1e300)) return PT_MPROF(lin_fail_zero), 0;  // zero, inf, NaN
+    const int e = ilogb(x);
     if (e < -960) return 0;  // stay clear of subnormals
-    double q = ldexp(c, 52 - e);  // c / u, exact (power-of-two scaling)
-    if (!(fabs(q) < 4.0e15)) return 0;  // |c| >= 2^52 u: leaves the binade at once
-    int64_t X = (int64_t)ldexp(x, 52 - e);
-    double qf = floor(q);
-    int64_t R;
+    const double sc = ldexp(1.0, 52 - e);  // 1/u, a power of two: scaling by it is exact
+    const double q = c * sc;               // c / u
+    if (!(fabs(q) < 4.0e15)) return PT_MPROF(lin_fail_q), 0;  // |c| >= 2^52 u: leaves the binade at once
+    const double X = x * sc;               // integer, 2^52 <= |X| < 2^53
+    const double qf = floor(q);
+    double R;
     if (q - qf == 0.5) {
         // Round-half-even tie: x + c sits halfway between two grid points and
         // rounds to the even one.  From an even X the sum lands on an even X
         // again, advancing by the even one of {k, k+1} every step.
-        if (X & 1) return 0;  // one literal step first makes X even
-        int64_t k = (int64_t)qf;
-        R = (k & 1) ? k + 1 : k;
+        if (floor(X * 0.5) * 2.0 != X) return PT_MPROF(lin_fail_tie), 0;  // one literal step first makes X even
+        R = floor(qf * 0.5) * 2.0 == qf ? qf : qf + 1.0;
     } else {
-        R = (int64_t)rint(q);
+        R = rint(q);
     }
-    int64_t C = (int64_t)ceil(fabs(q));
-    const int64_t lo = ((int64_t)1 << 52) + C + 1, hi = ((int64_t)1 << 53) - C - 1;
-    int64_t A = X >= 0 ? X : -X, Rs = X >= 0 ? R : -R;
-    if (A < lo || A > hi) return 0;
+    const double C = ceil(fabs(q));
+    const double lo = 4503599627370496.0 + C + 1.0, hi = 9007199254740992.0 - C - 1.0;
+    const double A = fabs(X), Rs = X >= 0.0 ? R : -R;
+    if (A < lo || A > hi) return PT_MPROF(lin_fail_zone), 0;
     L->X = X;
     L->R = R;
-    L->sh = e - 52;
-    if (Rs == 0) return BIG;
-    // room = floor(span / |Rs|) without a (software) int64 division: both are
-    // integers < 2^53, exact in f64; the rounded quotient is off by at most one.
-    int64_t span = Rs > 0 ? hi - A : A - lo, step = Rs > 0 ? Rs : -Rs;
-    int64_t room = (int64_t)floor((double)span / (double)step);
-    if (room * step > span) room--;
-    else if ((room + 1) * step <= span) room++;
-    return room + 1 < BIG ? room + 1 : BIG;
+    L->u = 1.0 / sc;  // exact
+    if (Rs == 0.0) return BIG;
+    const double span = Rs > 0.0 ? hi - A : A - lo, step = fabs(Rs);
+    if (span >= BIGD * step) return BIG;
+    return (int64_t)floor_div(span, step) + 1;
 }
 
 PT_HD double lin_at(const Lin &L, double x, int64_t j) {
     if (L.frozen) return x;
-    return ldexp((double)(L.X + j * L.R), L.sh);
+    return (L.X + (double)j * L.R) * L.u;
 }
 
 // x after n literal additions fl(x + c), exactly, across any number of binade
@@ -134,6 +169,7 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
 // others, so p, t can be advanced separately.
 PT_HD double advance(double x, double c, int64_t n) {
     while (n > 0) {
+        PT_MPROF(advance_loops);
         Lin L;
         int64_t room = lin_init(x, c, &L);
         if (room >= 2) {
@@ -148,19 +184,51 @@ PT_HD double advance(double x, double c, int64_t n) {
     return x;
 }
 
+// A lower bound on steps_in_range, in closed form: every add rounds by at
+// most delta = 2^-53 max(|start|, |end|) while t stays in range, so
+// t_j <= t + j (s + delta) (s > 0; mirrored for s < 0) and all j with
+// j <= (lim - t) / (|s| + delta) are in range; the quotient is shrunk by a
+// relative 1e-12 and one step for its own rounding.  Blocks only need a
+// lower bound: the last few steps before the range end are taken literally.
+PT_HD int64_t steps_in_range_lb(double t, double s, double start, double end, int64_t cap) {
+    const double lim = s > 0.0 ? end : start;
+    const double dist = s > 0.0 ? end - t : t - start;
+    if (!(dist >= 0.0)) return 0;
+    const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
+    const double k = floor(dist / (fabs(s) + delta) * (1.0 - 1e-12)) - 1.0;
+    (void)lim;
+    if (!(k >= 0.0)) return 1;
+    return k + 1.0 >= (double)cap ? cap : (int64_t)k + 1;
+}
+
 // Largest b (<= cap) such that t_0 .. t_{b-1} of t_{j+1} = fl(t_j + s) all lie
 // in [start, end] (the reference's check before each step), given t_0 does.
+// Closed form per binade segment of t: t_k = (X + kR) u stays in range while
+// k <= D / |R|, D the grid distance to the limit.
 PT_HD int64_t steps_in_range(double t, double s, double start, double end, int64_t cap) {
-    double lim = s > 0.0 ? end : start;
-    double est = (lim - t) / s;  // >= 0
-    int64_t k = est >= (double)cap ? cap : (int64_t)est;  // candidate last index
-    auto inside = [&](int64_t j) {
-        double tj = advance(t, s, j);
-        return !(tj > end || tj < start);
-    };
-    while (k > 0 && !inside(k)) k--;
-    while (k + 1 < cap && inside(k + 1)) k++;
-    return k + 1;
+    int64_t j0 = 0;  // index of x = t_j0, in range
+    double x = t;
+    for (;;) {
+        PT_MPROF(sir_inside);
+        Lin L;
+        const int64_t room = lin_init(x, s, &L);
+        if (room >= 2 && !L.frozen) {
+            const int64_t B = imin(room, cap - 1 - j0);  // points x_0 .. x_B of the segment
+            const double sc = 1.0 / L.u;
+            const double D = s > 0.0 ? floor(end * sc) - L.X : L.X - ceil(start * sc);
+            const double aR = fabs(L.R);
+            const int64_t k = D >= aR * (double)B ? B : (int64_t)floor_div(D, aR);
+            if (k < B || j0 + B >= cap - 1) return j0 + k + 1;
+            j0 += B;
+            x = lin_at(L, x, B);
+        } else {
+            if (L.frozen) return cap;  // s == 0 never leaves
+            const double y = x + s;
+            if (y > end || y < start) return j0 + 1;
+            x = y;
+            if (++j0 >= cap - 1) return cap;
+        }
+    }
 }
 
 // ------------------------------------------------ polynomial sign proof
@@ -170,6 +238,9 @@ PT_HD int64_t steps_in_range(double t, double s, double start, double end, int64
 // exact arithmetic.  heart_poly computes its coefficients; the bound below
 // proves that every f64 evaluation of heart_f at p_1..p_B keeps one sign and
 // stays clear of the 1e-15 stop.
+#ifndef PT_NEWTON
+#define PT_NEWTON 0
+#endif
 struct Poly {
     double g[7];                       // coefficients of g(j)
     double ax, ay, az, cx, cy, cz;     // |p0|, |ch| for the magnitude bound
@@ -226,7 +297,7 @@ PT_HD double poly_mag(const Poly &P, double b) {
     return am * am * am + x2 * z3 + 0.1125 * y2 * z3;
 }
 
-PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
+PT_HD double poly_margin(const Poly &P, double b) {
     const double e256 = 2.8421709430404007e-14;  // 256 * 2^-53
     double mag = poly_mag(P, b);
     // The step points are p_j = p0 + j*c + delta_j with |delta_j,k| <= j*ulp_k/2
@@ -238,40 +309,159 @@ PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
     double gy = 13.5 * ym * am2 + 0.225 * ym * z3;
     double gz = 6.0 * zm * am2 + 3.0 * x2 * z2 + 0.3375 * y2 * z2;
     double drift = b * 2.3e-16 * (gx * xm + gy * ym + gz * zm);  // ulp(v)/2 <= 2^-53 |v| (2.3e-16 > 2^-52)
-    double margin = 1e-15 + e256 * mag + drift;
-    double g0 = sgn * P.g[0], g1 = sgn * P.g[1];
-    if (g0 <= margin) return false;
-    // derivative remainder sum_{k>=2} k |g_k| b^(k-1)
-    double d1 = 0.0;
-    for (int k = 6; k >= 2; k--) d1 = d1 * b + k * fabs(P.g[k]);
-    d1 *= b;
-    if (fabs(g1) - d1 > e256 * 6.0 * mag / b) {
-        if (g1 > 0.0) return true;  // increasing away from zero: min is g(0+) > g0 > margin
-        double gb = 0.0;            // decreasing: the minimum is g(b)
-        for (int k = 6; k >= 0; k--) gb = gb * b + sgn * P.g[k];
-        return gb > margin;
-    }
-    double d = 0.0;
-    for (int k = 6; k >= 1; k--) d = (d + fabs(P.g[k])) * b;
-    return g0 - d > margin;
+    return 1e-15 + e256 * mag + drift;
 }
 
-// Predicted first crossing (in steps) from the quadratic part of sgn*g; the
-// search starts there and the proof decides.
+// Bernstein form of sgn*g on j in [0, b] (lambda = j / b): g >= min_i beta_i
+// over the whole block (convex hull property), and min beta = g(b) exactly
+// when the control polygon is monotone, so the test is tight for the usual
+// monotone approach to the surface.  The betas' own rounding (weights <= 1,
+// at most 7 terms) is far inside the 256 eps M(b) part of the margin.
+PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
+    const double margin = poly_margin(P, b);
+    double a[7];
+    double bk = 1.0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        a[k] = sgn * P.g[k] * bk;
+        bk *= b;
+    }
+    if (a[0] <= margin) return false;
+    const double b1 = a[0] + a[1] * (1.0 / 6.0);
+    const double b2 = a[0] + a[1] * (1.0 / 3.0) + a[2] * (1.0 / 15.0);
+    const double b3 = a[0] + a[1] * 0.5 + a[2] * 0.2 + a[3] * 0.05;
+    const double b4 = a[0] + a[1] * (2.0 / 3.0) + a[2] * 0.4 + a[3] * 0.2 + a[4] * (1.0 / 15.0);
+    const double b5 = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
+    const double b6 = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
+    const double mn = fmin(fmin(fmin(b1, b2), fmin(b3, b4)), fmin(b5, b6));
+    return mn > margin;
+}
+
+// Longest provable prefix of a block: the largest integer b <= B such that
+// sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither the
+// approx_equal stop nor a sign change can fire before step b).  One Bernstein
+// form on [0, B], then de Casteljau halving toward the first region the hull
+// cannot clear: each level either proves the left half (and moves right) or
+// descends into it.  The margin is the one for the whole block (M and the
+// drift only grow with b), and the halving's own rounding (<= 24 levels of
+// exact-weight averages) stays far inside its 256 eps M part.
+PT_HD int64_t poly_prefix(const Poly &P, int64_t B, double sgn) {
+    const double Bd = (double)B;
+    const double margin = poly_margin(P, Bd);
+    double a[7];
+    double bk = 1.0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        a[k] = sgn * P.g[k] * bk;
+        bk *= Bd;
+    }
+    if (a[0] <= margin) return 0;
+    double c[7];
+    c[0] = a[0];
+    c[1] = a[0] + a[1] * (1.0 / 6.0);
+    c[2] = a[0] + a[1] * (1.0 / 3.0) + a[2] * (1.0 / 15.0);
+    c[3] = a[0] + a[1] * 0.5 + a[2] * 0.2 + a[3] * 0.05;
+    c[4] = a[0] + a[1] * (2.0 / 3.0) + a[2] * 0.4 + a[3] * 0.2 + a[4] * (1.0 / 15.0);
+    c[5] = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
+    c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
+    double lo = 0.0, len = 1.0, proven = 0.0;  // in units of B
+    for (int level = 0; level < 40; level++) {
+        PT_MPROF(evals);
+        double mn = fmin(fmin(fmin(c[1], c[2]), fmin(c[3], c[4])), fmin(fmin(c[5], c[6]), c[0]));
+        if (mn > margin) {
+            proven = lo + len;
+            break;
+        }
+        if (len * Bd < 1.0) break;  // narrower than one step: nothing more to prove here
+        // de Casteljau at 1/2 in place: level r overwrites c[0 .. 6-r], so
+        // afterwards c[i] is the level-(6-i) point i = the right half's
+        // control point i; the left half's are the levels' first points.
+        double l[7];
+        l[0] = c[0];
+#pragma unroll
+        for (int r = 1; r < 7; r++) {
+#pragma unroll
+            for (int i = 0; i < 7 - r; i++) c[i] = (c[i] + c[i + 1]) * 0.5;
+            l[r] = c[0];
+        }
+        double mnl = fmin(fmin(fmin(l[1], l[2]), fmin(l[3], l[4])), fmin(fmin(l[5], l[6]), l[0]));
+        len *= 0.5;
+        if (mnl > margin) {
+            proven = lo + len;
+            lo += len;  // continue in the right half (c)
+        } else {
+            for (int i = 0; i < 7; i++) c[i] = l[i];
+        }
+    }
+    double b = floor(proven * Bd);
+    return b < 0.0 ? 0 : (int64_t)b;
+}
+
+// Predicted first crossing (in steps) of sgn*g: the quadratic part's first
+// positive root, polished by Newton steps on the full polynomial; the search
+// starts just before it and the proof decides.
+PT_HD double poly_eval(const Poly &P, double j, double *dg) {
+    double g = P.g[6], d = 0.0;
+#pragma unroll
+    for (int k = 5; k >= 0; k--) {
+        d = d * j + g;
+        g = g * j + P.g[k];
+    }
+    *dg = d;
+    return g;
+}
+
 PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
     double L = sgn * P.g[0], S = sgn * P.g[1], Q = sgn * P.g[2];
     if (L <= 0.0) return 1.0;
-    if (Q == 0.0) return S < 0.0 ? fmin(cap, L / -S) : cap;
-    double disc = S * S - 4.0 * Q * L;
-    if (disc < 0.0) return cap;  // no real root of the quadratic
-    double sq = sqrt(disc);
-    double r1 = (-S - sq) / (2.0 * Q), r2 = (-S + sq) / (2.0 * Q);
-    double lo = fmin(r1, r2), hi = fmax(r1, r2);
-    double r = lo > 0.0 ? lo : (hi > 0.0 ? hi : cap);
-    return fmin(cap, r);
+    double r;
+    if (Q == 0.0) {
+        r = S < 0.0 ? L / -S : cap;
+    } else {
+        double disc = S * S - 4.0 * Q * L;
+        if (disc < 0.0) {
+            r = cap;  // no real root of the quadratic
+        } else {
+            double sq = sqrt(disc);
+            double r1 = (-S - sq) / (2.0 * Q), r2 = (-S + sq) / (2.0 * Q);
+            double lo = fmin(r1, r2), hi = fmax(r1, r2);
+            r = lo > 0.0 ? lo : (hi > 0.0 ? hi : cap);
+        }
+    }
+    r = fmin(cap, r);
+#pragma unroll
+    for (int it = 0; it < PT_NEWTON; it++) {
+        double d, g = poly_eval(P, r, &d);
+        if (!(d != 0.0)) break;
+        double nr = r - g / d;
+        if (!(nr > 0.0)) break;
+        r = fmin(cap, nr);
+    }
+    return r;
 }
 
 // ------------------------------------------------------- the march
+#ifndef PT_SEARCH_DIV
+#define PT_SEARCH_DIV 4
+#endif
+#ifndef PT_SEARCH_START
+#define PT_SEARCH_START 0.999
+#endif
+#ifndef PT_SEARCH_DESCENT
+#define PT_SEARCH_DESCENT 10
+#endif
+#ifndef PT_SEARCH_REFINE
+#define PT_SEARCH_REFINE 10
+#endif
+#ifndef PT_MIN_GUESS
+#define PT_MIN_GUESS 2.0
+#endif
+#ifndef PT_BLOCK_SCALE
+#define PT_BLOCK_SCALE 1.25
+#endif
+#ifndef PT_BLOCK_PAD
+#define PT_BLOCK_PAD 4
+#endif
 struct MarchStats {
     uint32_t steps, blocks, tries;
 };
@@ -281,15 +471,19 @@ struct MarchStats {
 // the other lanes of its wave keep tracing.
 struct MarchState {
     double t, px, py, pz, r, s, start, end, dx, dy, dz;
+    int64_t lim;  // steps_in_range from the current point for this pass (-1: not known yet)
     int pass, passes;
+    uint32_t iters;  // guard: a march that has not ended after MARCH_GUARD iterations is dropped
 };
 enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2 };
+constexpr uint32_t MARCH_GUARD = 1u << 24;
 
 // Bound test and start of the march; false if the ray misses the bound.
 PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
                        MarchState *m) {
     double start, end;
     if (!heart_bound(ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+    PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz);
     m->start = start;
     m->end = end;
     m->s = step0;
@@ -303,6 +497,8 @@ PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz
     m->dz = dz;
     m->pass = 0;
     m->passes = passes;
+    m->lim = -1;
+    m->iters = 0;
     return true;
 }
 
@@ -311,53 +507,48 @@ PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz
 // t-in-[min_t, max_t] test); M_MISS: t left [start, end].
 template <bool STATS>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
+    PT_MPROF(iters);
     if (m.pass >= m.passes) return M_DONE;
+    // Every iteration takes >= 1 reference step; a march still running after
+    // 2^24 of them is one the reference itself would not finish (a step below
+    // t's rounding, say).  Dropping it keeps every GPU wave finite.
+    if (++m.iters > MARCH_GUARD) return M_MISS;
     if (m.t > m.end || m.t < m.start) return M_MISS;
     double s = m.s;
     double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
     // ---- try to jump a block of b steps (exact advance + sign proof)
     if (m.r != 0.0) {
-        int64_t bmax = steps_in_range(m.t, s, m.start, m.end, (int64_t)1 << 24);
+        // the range limit moves with the sequence: computed once per pass
+        if (m.lim < 0) m.lim = steps_in_range_lb(m.t, s, m.start, m.end, (int64_t)1 << 24);
+        const int64_t bmax = m.lim;
         if (bmax >= 2) {
             Poly P;
             heart_poly(m.px, m.py, m.pz, cx, cy, cz, &P);
             if (STATS) st->tries++;
-            // largest provable block: start at the predicted crossing, drop by
-            // 4x until proven, then refine upward (gallop / bisect)
-            double sgn = m.r > 0.0 ? 1.0 : -1.0;
-            double guess = poly_root_guess(P, sgn, (double)bmax);
-            int64_t good = 0, bad = bmax + 1;
-            int64_t b = (int64_t)(guess * 0.999);
-            b = b < 2 ? 2 : (b > bmax ? bmax : b);
-            int evals = 0;
-            while (b >= 2 && evals < 10) {
-                evals++;
-                if (poly_sign_definite(P, (double)b, sgn)) {
-                    good = b;
-                    break;
-                }
-                bad = b;
-                b >>= 2;
-            }
-            while (good >= 2 && evals < 10 && bad - good > 1 + good / 16) {
-                b = bad > bmax ? (2 * good > bmax ? bmax : 2 * good) : good + (bad - good) / 2;
-                if (b <= good || b >= bad) break;
-                evals++;
-                if (poly_sign_definite(P, (double)b, sgn)) good = b;
-                else bad = b;
-            }
+            // longest provable prefix of a block sized from the predicted
+            // crossing (the margin scales with the block, so a block far
+            // longer than the crossing distance would drown the near part)
+            const double sgn = m.r > 0.0 ? 1.0 : -1.0;
+            const double guess = poly_root_guess(P, sgn, (double)bmax);
+            if (guess < PT_MIN_GUESS) goto literal;  // the crossing is the next step or two
+            int64_t B = (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
+            B = B > bmax ? bmax : (B < 2 ? 2 : B);
+            const int64_t good = poly_prefix(P, B, sgn);
             if (good >= 2) {
                 m.t = advance(m.t, s, good);
                 m.px = advance(m.px, cx, good);
                 m.py = advance(m.py, cy, good);
                 m.pz = advance(m.pz, cz, good);
                 m.r = heart_f(m.px, m.py, m.pz);
+                m.lim -= good;
                 if (STATS) st->blocks++;
                 return M_RUNNING;
             }
         }
     }
+literal:
     // ---- one literal step (ray_marching.rs:37-51)
+    if (m.lim > 0) m.lim--;
     m.t += s;
     m.px += cx;
     m.py += cy;
@@ -371,6 +562,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
     if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
         m.s = s * -0.01;
         m.r = next;
+        m.lim = -1;
         m.pass++;
         return m.pass >= m.passes ? M_DONE : M_RUNNING;
     }

@@ -39,8 +39,6 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.nlin = (int)b->acc.lin.size();
         b->view.nmarch = (int)b->acc.march.size();
         b->view.diag = 0;
-        b->view.march_trigger = 1;
-        b->view.march_keep = 1;
         b->s11 = uniform_incl_scale(-1.0, 1.0);
         return b;
     } catch (...) {
@@ -101,4 +99,27 @@ extern "C" void h_trace_pixels(void *p, uint32_t w, uint32_t h, uint32_t spp, ui
                                : dev::trace_pixel<32>(b->view, P, pixels[i] % w, pixels[i] / w);
         out[3 * i] = c.x, out[3 * i + 1] = c.y, out[3 * i + 2] = c.z;
     }
+}
+
+// trace_pixel's STATS build on the host: the event counters pt_count_work
+// returns from the GPU, for an equality check.
+extern "C" void h_count_work(void *p, uint32_t w, uint32_t h, uint32_t spp, uint32_t depth, uint64_t seed,
+                             const uint32_t *pixels, size_t n, uint64_t *counters) {
+    Bundle *b = (Bundle *)p;
+    FrameParams P;
+    std::memset(&P, 0, sizeof P);
+    caster_params(b->sc.camera, w, h, &P);
+    P.s11 = b->s11;
+    P.seed = seed;
+    P.width = w;
+    P.height = h;
+    P.spp = spp;
+    P.depth = depth;
+    Ctr c;
+    std::memset(&c, 0, sizeof c);
+    for (size_t i = 0; i < n; i++) {
+        if (depth <= 8) dev::trace_pixel<4, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c);
+        else dev::trace_pixel<32, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c);
+    }
+    for (int k = 0; k < C_COUNT; k++) counters[k] = c.c[k];
 }

@@ -264,3 +264,59 @@ def test_wavefront_shards(pt, cornell):
     with _env(PT_ENGINE="mega"):
         want = r.render(cam, pt.ImageParams(w, h), spp, seed=8)
     assert np.array_equal(frame.cpu().numpy().reshape(-1, 3), want)
+
+
+def test_heart_march_many_rays(pt, cornell):
+    """Tens of thousands of rays through the Heart's bound (camera rays and
+    rays leaving its surface), closest hit on the GPU vs the oracle: catches
+    device-only numerics in the skipping march (hardware reciprocals etc.)."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    rng = np.random.default_rng(17)
+    n = 12000
+    eye = np.tile([278.0, 278.0, -800.0], (n, 1))
+    tgt = rng.uniform([120, 120, 60], [310, 280, 240], size=(n, 3))
+    d1 = tgt - eye
+    d1 /= np.linalg.norm(d1, axis=1, keepdims=True)
+    # origins on / near the Heart, random directions (bounce rays)
+    o2 = rng.uniform([150, 140, 90], [280, 260, 210], size=(n, 3))
+    d2 = rng.normal(size=(n, 3))
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    rays = np.concatenate([np.concatenate([eye, d1], 1), np.concatenate([o2, d2], 1)])
+    got = r.closest_hit(rays)
+    bad = 0
+    for i, ray in enumerate(rays):
+        h = osc.closest_hit(ray[:3], ray[3:])
+        g = got[i]
+        if h is None:
+            bad += g["shape"] != -1
+        else:
+            bad += not (g["shape"] == h.shape and g["t"] == h.t)
+    assert bad == 0, "%d of %d rays differ" % (bad, len(rays))
+
+
+def test_count_work_matches_host_build(pt, cornell, cornell_text):
+    """The GPU's STATS counters equal the host build's of the same code,
+    event for event (the FLOP side of the roofline rests on them)."""
+    import ctypes as C
+    import subprocess
+    from pathlib import Path
+    native = Path(__file__).resolve().parent / "native"
+    subprocess.run(["make", "-s", "-C", str(native)], check=True)
+    L = C.CDLL(str(native / "_build" / "libpath.so"))
+    L.h_scene_new.restype = C.c_void_p
+    L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]
+    L.h_count_work.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                               C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_uint64)]
+    raw = cornell_text.encode()
+    h = L.h_scene_new(raw, len(raw), 1, 1)
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    w, hh = 1920, 1080
+    rng = np.random.default_rng(9)
+    px = np.concatenate([rng.choice(w * hh, 200, replace=False),
+                         np.arange(64) * 12 + 1688069]).astype(np.uint32)
+    got = pt.count_work(r, ps.camera(), pt.ImageParams(w, hh), 4, px, seed=1)
+    want = (C.c_uint64 * len(pt.COUNTERS))()
+    L.h_count_work(h, w, hh, 4, 8, 1, px.ctypes.data_as(C.POINTER(C.c_uint32)), len(px), want)
+    assert got == dict(zip(pt.COUNTERS, list(want)))

@@ -32,6 +32,8 @@
 // bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include <cstdlib>
 
 #include "pt_device.hpp"
@@ -50,8 +52,9 @@ struct WfView {
     uint32_t *meta;  // depth | stack count << 8
     uint64_t *stk;   // NW words per path, word k at stk[k * cap + id]
     double *rx, *ry, *rz;  // sample radiance of finished paths
-    uint32_t *list[2], *mq;
-    uint32_t *cnt;  // per iteration: [0] live count, [1] march count, [2] march head, [3] unused
+    uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
+    uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
+    uint32_t *cnt;  // per iteration: [0] live-list count, [1] march-queue count, [2..3] unused
     double *acc;    // running per-pixel sums (3 per pixel of the tile group)
     uint32_t cap;   // path slots
     uint32_t npix;  // pixels of the tile group (tiles * 256)
@@ -61,19 +64,6 @@ struct WfView {
 
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-
-// Wave-aggregated queue push: every active lane calls it; lanes with p get
-// consecutive slots (in lane order) from one atomic.
-__device__ __forceinline__ uint32_t wave_push(uint32_t *counter, bool p) {
-    const uint64_t m = __ballot(p);
-    if (m == 0) return 0;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    return base + below;
 }
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
@@ -92,14 +82,15 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
     *y = ty * TILE + (((w >> 1) << 3) | (l >> 3));
 }
 
+#ifndef PT_WF_BOUNCE_WAVES
+#define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
+#endif
+
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
-template <int NW, bool FIRST>
-__global__ __launch_bounds__(256) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it) {
+template <int NW, bool FIRST, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it) {
+    // input: the id-sorted list of live paths (iteration 0: every slot)
     const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
-    const uint32_t *lin_ = v.list[it & 1];
-    uint32_t *lout = v.list[(it + 1) & 1];
-    uint32_t *cnext = &v.cnt[(it + 1) * 4 + 0];
-    uint32_t *cmarch = &v.cnt[it * 4 + 1];
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         const uint32_t i = base + threadIdx.x;
@@ -123,7 +114,7 @@ __global__ __launch_bounds__(256) void wf_bounce(dev::Scene sc, FrameParams P, W
                     depth = P.depth;
                 }
             } else {
-                id = lin_[i];
+                id = v.list[i];
                 ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
                 ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
                 rng.s = v.rng[id];
@@ -172,95 +163,106 @@ __global__ __launch_bounds__(256) void wf_bounce(dev::Scene sc, FrameParams P, W
 #pragma unroll
             for (int k = 0; k < NW; k++) v.stk[(size_t)k * v.cap + id] = stk.w[k];
         }
-        const uint32_t qm = wave_push(cmarch, live && need_march);
-        if (live && need_march) v.mq[qm] = id;
-        const uint32_t qn = wave_push(cnext, live && !need_march);
-        if (live && !need_march) lout[qn] = id;
+        if (i < count) v.status[id] = live ? (need_march ? 3u : 1u) : 0u;
     }
 }
 
-// Marches of iteration `it`: persistent lanes, each refilled from the queue as
-// soon as its job is done.  A job is the select loop over the marched shapes
-// (trace_pixel's SELECT/MARCH phases) for one path; its result (best, who)
-// goes back to the path, which joins the next live list.
-__global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it) {
-    const uint32_t count = v.cnt[it * 4 + 1];
-    uint32_t *head = &v.cnt[it * 4 + 2];
-    uint32_t *cnext = &v.cnt[(it + 1) * 4 + 0];
-    uint32_t *lout = v.list[(it + 1) & 1];
-    bool busy = false, retired = false, marching = false;
-    uint32_t id = 0;
-    int km = 0, who = -1, mshape = -1;
-    double best = 0.0;
+// Order-preserving compaction of the status bytes into id lists (hipcub
+// select): neighbouring pixels stay in neighbouring lanes, so the next
+// kernels' structure-of-arrays loads stay coalesced and march waves coherent.
+struct StatusHas {
+    const uint8_t *st;
+    uint8_t bit;
+    __host__ __device__ bool operator()(const uint32_t &id) const { return (st[id] & bit) != 0; }
+};
+
+// Marches of iteration `it`.  Each workgroup owns a contiguous slice of the
+// march queue and hands jobs to its lanes through an LDS counter; every lane
+// keeps its next job's ray already loaded (the index one job further ahead)
+// so a lane that finishes starts the next march without waiting on memory.
+// A job is trace_pixel's SELECT/MARCH loop over the marched shapes for one
+// path; (best, who) go back to the path, which the next bounce kernel reads
+// straight from this queue.
+struct MarchJob {
+    uint32_t id;
     Ray ray;
-    V3 inv = dev::v3(0.0, 0.0, 0.0);
+    double best;
+    int who;
+};
+
+__device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob *j) {
+    j->id = id;
+    j->ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
+    j->ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
+    j->best = v.t[id];
+    j->who = v.who[id];
+}
+
+__global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it) {
+    __shared__ uint32_t head;
+    const uint32_t count = v.cnt[it * 4 + 1];
+    const uint32_t *mq = v.mq;
+    const uint32_t per = (count + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = blockIdx.x * per, hi = min(count, lo + per);
+    if (threadIdx.x == 0) head = lo + blockDim.x;
+    __syncthreads();
+    // current job (slot lo + thread), next job (state in flight), index after next
+    uint32_t q = lo + threadIdx.x;
+    bool have = q < hi;
+    MarchJob cur, nxt;
+    if (have) load_job(v, mq[q], &cur);
+    uint32_t qn = have ? atomicAdd(&head, 1u) : hi;
+    bool nhave = qn < hi;
+    if (nhave) load_job(v, mq[qn], &nxt);
+    uint32_t q2 = nhave ? atomicAdd(&head, 1u) : hi;
+    uint32_t id2 = q2 < hi ? mq[q2] : 0u;
+    bool marching = false;
+    int km = 0, mshape = -1;
+    V3 inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchState ms;
     march::MarchStats mst{0, 0, 0};
-    for (;;) {
-        // refill idle lanes with one atomic per wave
-        const bool want = !busy && !retired;
-        const uint64_t m = __ballot(want);
-        if (m != 0) {
-            const int leader = __ffsll((long long)m) - 1;
-            uint32_t base = 0;
-            if ((int)lane_id() == leader) base = atomicAdd(head, (uint32_t)__popcll(m));
-            base = __shfl(base, leader, 64);
-            if (want) {
-                const uint32_t q =
-                    base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                if (q < count) {
-                    id = v.mq[q];
-                    ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
-                    ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
-                    inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-                    best = v.t[id];
-                    who = v.who[id];
-                    km = 0;
-                    marching = false;
-                    busy = true;
-                } else {
-                    retired = true;
-                }
-            }
-        }
-        if (__ballot(busy) == 0) break;  // queue drained and no lane holds a job
+    while (have) {
         bool done = false;
-        if (busy) {
-            if (marching) {
-                const int st = march::march_iter<false>(ms, &mst);
-                if (st != march::M_RUNNING) {
-                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
-                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
-                        best = ms.t;
-                        who = mshape;
-                    }
-                    marching = false;
+        if (marching) {
+            const int st = march::march_iter<false>(ms, &mst);
+            if (st != march::M_RUNNING) {
+                // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
+                if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
+                    (ms.t < cur.best || mshape > cur.who)) {
+                    cur.best = ms.t;
+                    cur.who = mshape;
                 }
-            } else {
-                // select: next marched shape whose bound is entered before `best`
-                while (km < sc.nmarch) {
-                    const int s = sc.march[km++];
-                    const DBox &b = sc.boxes[s];
-                    if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
-                    const DShape &S = sc.shapes[s];
-                    const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
-                    if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                        mshape = s;
-                        marching = true;
-                        break;
-                    }
-                }
-                if (!marching) {
-                    v.t[id] = best;
-                    v.who[id] = who;
-                    done = true;
+                marching = false;
+            }
+        } else {
+            // select: next marched shape whose bound is entered before `best`
+            while (km < sc.nmarch) {
+                const int s = sc.march[km++];
+                const DBox &b = sc.boxes[s];
+                if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                const DShape &S = sc.shapes[s];
+                const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                    mshape = s;
+                    marching = true;
+                    break;
                 }
             }
+            done = !marching;
         }
-        const uint32_t qn = wave_push(cnext, done);
         if (done) {
-            lout[qn] = id;
-            busy = false;
+            v.t[cur.id] = cur.best;
+            v.who[cur.id] = cur.who;
+            have = nhave;
+            if (have) {
+                cur = nxt;
+                inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
+                km = 0;
+                nhave = q2 < hi;
+                if (nhave) load_job(v, id2, &nxt);
+                q2 = nhave ? atomicAdd(&head, 1u) : hi;
+                id2 = q2 < hi ? mq[q2] : 0u;
+            }
         }
     }
 }
@@ -299,7 +301,16 @@ __global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int fi
 }
 
 // ------------------------------------------------------------- host driver
-static size_t path_bytes(int nw) { return 7 * 8 + 8 + 4 + 4 + (size_t)nw * 8 + 3 * 8 + 3 * 4; }
+static size_t path_bytes(int nw) { return 7 * 8 + 8 + 4 + 4 + (size_t)nw * 8 + 3 * 8 + 2 * 4 + 1; }
+
+// temp storage of one select over n slots
+static size_t select_bytes(uint32_t n) {
+    size_t b = 0;
+    StatusHas pred{nullptr, 1};
+    (void)hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), (uint32_t *)nullptr,
+                                   (uint32_t *)nullptr, (int64_t)n, pred, (hipStream_t)0);
+    return b;
+}
 
 static uint32_t wf_cap_paths() {
     const char *e = getenv("PT_WF_PATHS");
@@ -325,6 +336,26 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
     return hipSuccess;
 }
 
+static int bounce_waves() {
+    const char *e = getenv("PT_WF_BOUNCE_WAVES");
+    const int w = e ? atoi(e) : PT_WF_BOUNCE_WAVES;
+    return w >= 2 && w <= 4 ? w : PT_WF_BOUNCE_WAVES;
+}
+
+template <int NW, bool FIRST>
+static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
+                          const WfView &v, int it) {
+    if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
+        wf_bounce<NW, FIRST, 2><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        return;
+    }
+    switch (bounce_waves()) {
+    case 2: wf_bounce<NW, FIRST, 2><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 4: wf_bounce<NW, FIRST, 4><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    default: wf_bounce<NW, FIRST, 3><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    }
+}
+
 template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws) {
@@ -340,7 +371,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const uint32_t cap = ns * npix_max;
     const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
     const size_t cnt_words = (size_t)(iters + 2) * 4;
-    const size_t bytes = (size_t)cap * path_bytes(NW) + (size_t)npix_max * 24 + cnt_words * 4 + 1024;
+    const size_t sel_bytes = select_bytes(cap);
+    const size_t bytes = (size_t)cap * path_bytes(NW) + (size_t)npix_max * 24 + cnt_words * 4 + sel_bytes + 4096;
     hipError_t e = reserve(ws, bytes);
     if (e != hipSuccess) return e;
     // carve the workspace
@@ -365,9 +397,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     v.rx = (double *)take((size_t)cap * 8);
     v.ry = (double *)take((size_t)cap * 8);
     v.rz = (double *)take((size_t)cap * 8);
-    v.list[0] = (uint32_t *)take((size_t)cap * 4);
-    v.list[1] = (uint32_t *)take((size_t)cap * 4);
+    v.list = (uint32_t *)take((size_t)cap * 4);
     v.mq = (uint32_t *)take((size_t)cap * 4);
+    v.status = (uint8_t *)take((size_t)cap);
+    void *sel_tmp = take(sel_bytes);
     v.acc = (double *)take((size_t)npix_max * 24);
     v.cnt = (uint32_t *)take(cnt_words * 4);
     if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
@@ -381,6 +414,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         }
         int occ = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march, 256, 0) == hipSuccess && occ > 0) per = occ;
+        const char *e = getenv("PT_WF_MARCH_BLOCKS_PER_CU");  // tuning knob
+        if (e && atoi(e) > 0 && atoi(e) < per) per = atoi(e);
         return (uint32_t)(cus * per);
     }();
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
@@ -397,17 +432,25 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             uint32_t bb = (paths + 255) / 256;
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
-            wf_bounce<NW, true><<<(paths + 255) / 256, 256, 0, st>>>(sc, P0, v, 0);
+            launch_bounce<NW, true>((paths + 255) / 256, st, sc, P0, v, 0);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
-                    wf_bounce<NW, false><<<bb, 256, 0, st>>>(sc, P0, v, it);
+                    launch_bounce<NW, false>(bb, st, sc, P0, v, it);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                 }
-                if (it < iters - 1) {
-                    wf_march<<<march_blocks, 256, 0, st>>>(sc, v, it);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
-                }
+                if (it == iters - 1) break;  // the last bounce only shades
+                // live list for it + 1 and march queue for it, both id-sorted
+                size_t tb = sel_bytes;
+                e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.list,
+                                             &v.cnt[(it + 1) * 4 + 0], (int64_t)paths, StatusHas{v.status, 1}, st);
+                if (e != hipSuccess) return e;
+                tb = sel_bytes;
+                e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.mq,
+                                             &v.cnt[it * 4 + 1], (int64_t)paths, StatusHas{v.status, 2}, st);
+                if (e != hipSuccess) return e;
+                wf_march<<<march_blocks, 256, 0, st>>>(sc, v, it);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             wf_reduce<<<(v.npix + 255) / 256, 256, 0, st>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;

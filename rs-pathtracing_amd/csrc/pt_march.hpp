@@ -35,6 +35,9 @@
 #ifndef PT_MPROF
 #define PT_MPROF(field) ((void)0)
 #endif
+#ifndef PT_MHOOK
+#define PT_MHOOK(what) ((void)0)
+#endif
 #ifndef PT_MCAPTURE
 #define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz) ((void)0)
 #endif
@@ -145,10 +148,13 @@ PT_HD int64_t lin_init(double x, double c, Lin *L) {
     } else {
         R = rint(q);
     }
+    // Only the binade edge the sequence moves toward matters: moving away from
+    // zero (Rs > 0) every exact sum A + |q| must stay below 2^53, moving toward
+    // it (Rs < 0) every A - |q| at or above 2^52 (then the sum rounds on grid u).
     const double C = ceil(fabs(q));
     const double lo = 4503599627370496.0 + C + 1.0, hi = 9007199254740992.0 - C - 1.0;
     const double A = fabs(X), Rs = X >= 0.0 ? R : -R;
-    if (A < lo || A > hi) return PT_MPROF(lin_fail_zone), 0;
+    if (Rs > 0.0 ? A > hi : (Rs < 0.0 && A < lo)) return PT_MPROF(lin_fail_zone), 0;
     L->X = X;
     L->R = R;
     L->u = 1.0 / sc;  // exact
@@ -168,6 +174,7 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
 // edge (and near zero).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
 PT_HD double advance(double x, double c, int64_t n) {
+    PT_MHOOK(adv_begin);
     while (n > 0) {
         PT_MPROF(advance_loops);
         Lin L;
@@ -176,11 +183,16 @@ PT_HD double advance(double x, double c, int64_t n) {
             int64_t k = room < n ? room : n;
             x = lin_at(L, x, k);
             n -= k;
+            if (n > 0 && k == room) {  // the add that leaves the segment: literal
+                x = x + c;
+                n--;
+            }
         } else {
             x = x + c;
             n--;
         }
     }
+    PT_MHOOK(adv_end);
     return x;
 }
 
@@ -365,6 +377,7 @@ PT_HD int64_t poly_prefix(const Poly &P, int64_t B, double sgn) {
     c[5] = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
     c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
     double lo = 0.0, len = 1.0, proven = 0.0;  // in units of B
+    PT_MHOOK(lv_begin);
     for (int level = 0; level < 40; level++) {
         PT_MPROF(evals);
         double mn = fmin(fmin(fmin(c[1], c[2]), fmin(c[3], c[4])), fmin(fmin(c[5], c[6]), c[0]));
@@ -393,6 +406,7 @@ PT_HD int64_t poly_prefix(const Poly &P, int64_t B, double sgn) {
             for (int i = 0; i < 7; i++) c[i] = l[i];
         }
     }
+    PT_MHOOK(lv_end);
     double b = floor(proven * Bd);
     return b < 0.0 ? 0 : (int64_t)b;
 }
@@ -535,10 +549,12 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             B = B > bmax ? bmax : (B < 2 ? 2 : B);
             const int64_t good = poly_prefix(P, B, sgn);
             if (good >= 2) {
+                PT_MHOOK(block_begin);
                 m.t = advance(m.t, s, good);
                 m.px = advance(m.px, cx, good);
                 m.py = advance(m.py, cy, good);
                 m.pz = advance(m.pz, cz, good);
+                PT_MHOOK(block_end);
                 m.r = heart_f(m.px, m.py, m.pz);
                 m.lim -= good;
                 if (STATS) st->blocks++;

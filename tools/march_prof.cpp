@@ -20,11 +20,21 @@ struct Job {
 };
 static std::vector<Job> g_jobs;
 static bool g_capture = false;
+static long g_hist_adv[64], g_hist_blockmax[64], g_hist_levels[64];
+static int g_cur_adv = 0, g_block_max = 0, g_cur_levels = 0;
 struct Prof {
     unsigned long long lin_init, advance_loops, sir_inside, evals, iters, lin_fail_zero, lin_fail_q, lin_fail_tie, lin_fail_zone;
 };
 static Prof g_prof;
 #define PT_MPROF(f) (g_prof.f++)
+#define PT_MHOOK(what) hook_##what()
+static unsigned long long g_adv0, g_lv0;
+static void hook_adv_begin();
+static void hook_adv_end();
+static void hook_lv_begin();
+static void hook_lv_end();
+static void hook_block_begin();
+static void hook_block_end();
 #define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz)                              \
     do {                                                                                 \
         if (g_capture) g_jobs.push_back(Job{step0, passes, 0, {ox, oy, oz}, {dx, dy, dz}}); \
@@ -35,6 +45,20 @@ static Prof g_prof;
 #include "../rs-pathtracing_amd/csrc/pt_scene.hpp"
 
 using namespace pt;
+
+static void hook_adv_begin() { g_adv0 = g_prof.advance_loops; }
+static void hook_adv_end() {
+    long k = (long)(g_prof.advance_loops - g_adv0);
+    g_hist_adv[k < 63 ? k : 63]++;
+    if (k > g_block_max) g_block_max = (int)k;
+}
+static void hook_lv_begin() { g_lv0 = g_prof.evals; }
+static void hook_lv_end() {
+    long k = (long)(g_prof.evals - g_lv0);
+    g_hist_levels[k < 63 ? k : 63]++;
+}
+static void hook_block_begin() { g_block_max = 0; }
+static void hook_block_end() { g_hist_blockmax[g_block_max < 63 ? g_block_max : 63]++; }
 
 // The reference march, literally (ray_marching.rs:20-74), in object space.
 static bool literal_march(const Job &j, double *t_out, long *steps) {
@@ -204,6 +228,17 @@ int main(int argc, char **argv) {
             }
             fclose(o);
         }
+        auto ph = [](const char *name, long *h) {
+            long tot = 0, w = 0;
+            for (int i = 0; i < 64; i++) tot += h[i], w += (long)i * h[i];
+            printf("%s (mean %.2f):", name, tot ? (double)w / tot : 0.0);
+            for (int i = 0; i < 64; i++)
+                if (h[i]) printf(" %d:%ld", i, h[i]);
+            printf("\n");
+        };
+        ph("advance loops per call", g_hist_adv);
+        ph("max advance loops over the 4 coords of a block", g_hist_blockmax);
+        ph("prefix levels per call", g_hist_levels);
         printf("iterations histogram:");
         for (int i = 0; i < 64; i++)
             if (hist[i]) printf(" %d:%d", i, hist[i]);

@@ -166,6 +166,12 @@ int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint3
  * Diagnostic / parity probe. */
 int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters);
 
+/* Diagnostic of the wavefront march kernel: returns (and clears) the counters
+ * accumulated since the last call into out[min(n, 36)] — trips and s_memtime
+ * cycles per mix of lane phases (16 + 16), lanes per phase (4) — and turns
+ * the instrumented build on (enable = 1) or off. */
+int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
+
 /* Diagnostic: render the whole frame (depth <= 8) with a timing build of the
  * megakernel and return wave-level s_memtime cycles summed over waves per
  * phase of its per-lane loop and pass counts: out[10] = {trace, march, select,

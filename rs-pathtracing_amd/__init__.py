@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
     "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
     "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_wave_diag", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -105,7 +105,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(str(LIB_PATH))
+    L = C.CDLL(os.environ.get("PT_AMD_LIB", str(LIB_PATH)))  # PT_AMD_LIB: an alternate build (tuning)
     vp, d = C.c_void_p, C.POINTER(C.c_double)
     u32, u64, sz = C.c_uint32, C.c_uint64, C.c_size_t
     sig = {
@@ -133,6 +133,7 @@ def lib():
                                     C.POINTER(u64)]),
         "pt_march_jobs": (C.c_int, [vp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                     C.POINTER(C.c_uint32)]),
+        "pt_wave_diag": (C.c_int, [vp, C.c_int, C.POINTER(u64), sz]),
         "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
         "pt_sample_key": (u64, [u64, u64, u64]),
@@ -140,6 +141,8 @@ def lib():
         "pt_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if "PT_AMD_LIB" in os.environ and not hasattr(L, name):
+            continue  # an older alternate build (tuning comparisons)
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -353,6 +356,13 @@ def march_jobs(renderer: "HipRenderer", jobs):
     _check(lib().pt_march_jobs(renderer._h, jobs.ctypes.data_as(dp), n, t.ctypes.data_as(dp),
                                st.ctypes.data_as(C.POINTER(C.c_int32)), it.ctypes.data_as(C.POINTER(C.c_uint32))))
     return t, st.astype(bool), it
+
+
+def wave_diag(renderer: "HipRenderer", enable: bool = True):
+    """Read-and-clear the wavefront march kernel's phase diagnostics (pt_wave_diag)."""
+    out = (C.c_uint64 * 36)()
+    _check(lib().pt_wave_diag(renderer._h, 1 if enable else 0, out, 36))
+    return list(out)
 
 
 def profile_phases(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,

@@ -453,6 +453,20 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
     return PT_OK;
 }
 
+int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
+    if (!r) return fail(PT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    if (out && n && r->ws.diag) HIP_TRY(hipMemcpy(out, r->ws.diag, (n < 36 ? n : 36) * 8, hipMemcpyDeviceToHost));
+    if (enable && !r->ws.diag) HIP_TRY(hipMalloc(&r->ws.diag, 36 * 8));
+    if (r->ws.diag) HIP_TRY(hipMemset(r->ws.diag, 0, 36 * 8));
+    if (!enable && r->ws.diag) {
+        HIP_TRY(hipFree(r->ws.diag));
+        r->ws.diag = nullptr;
+    }
+    return PT_OK;
+}
+
 int pt_profile_phases(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
                       uint64_t *out) {
     if (!r || !cam || !out) return fail(PT_ERR_INVALID, "null argument");

@@ -21,6 +21,7 @@ struct DeviceScene {
 struct WaveWorkspace {
     void *base = nullptr;
     size_t bytes = 0;
+    unsigned long long *diag = nullptr;  // march-kernel phase diagnostics (pt_wave_diag), when enabled
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

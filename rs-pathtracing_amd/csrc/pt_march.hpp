@@ -196,6 +196,25 @@ PT_HD double advance(double x, double c, int64_t n) {
     return x;
 }
 
+// One segment of advance(): the closed form to the end of x's binade segment
+// (and the literal add leaving it), or one literal add in an edge zone.
+PT_HD void seg_step(double &x, double c, double &n) {
+    Lin L;
+    const int64_t room = lin_init(x, c, &L);
+    if (room >= 2) {
+        const double k = (double)room < n ? (double)room : n;
+        x = lin_at(L, x, (int64_t)k);
+        n -= k;
+        if (n > 0.0 && k == (double)room) {
+            x = x + c;
+            n -= 1.0;
+        }
+    } else {
+        x = x + c;
+        n -= 1.0;
+    }
+}
+
 // A lower bound on steps_in_range, in closed form: every add rounds by at
 // most delta = 2^-53 max(|start|, |end|) while t stays in range, so
 // t_j <= t + j (s + delta) (s > 0; mirrored for s < 0) and all j with
@@ -211,6 +230,19 @@ PT_HD int64_t steps_in_range_lb(double t, double s, double start, double end, in
     (void)lim;
     if (!(k >= 0.0)) return 1;
     return k + 1.0 >= (double)cap ? cap : (int64_t)k + 1;
+}
+
+// An upper bound on the index J of the first t_J outside [start, end] (the
+// step at which the reference's range check ends the pass with a miss):
+// t_j >= t + j (s - delta) (s > 0; mirrored for s < 0), so J <= floor(dist /
+// (|s| - delta)) + 1; grown by a relative 1e-12 and two steps for rounding.
+PT_HD int64_t steps_exit_ub(double t, double s, double start, double end) {
+    const double dist = s > 0.0 ? end - t : t - start;
+    const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
+    const double as = fabs(s);
+    if (!(dist >= 0.0) || !(as > 2.0 * delta)) return BIG;
+    const double k = ceil(dist / (as - delta) * (1.0 + 1e-12)) + 2.0;
+    return k >= BIGD ? BIG : (int64_t)k;
 }
 
 // Largest b (<= cap) such that t_0 .. t_{b-1} of t_{j+1} = fl(t_j + s) all lie
@@ -470,6 +502,15 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
 #ifndef PT_MIN_GUESS
 #define PT_MIN_GUESS 2.0
 #endif
+#ifndef PT_ADV_ROUNDS
+#define PT_ADV_ROUNDS 64  // binade-segment rounds per march_advance call
+#endif
+#ifndef PT_EARLY_MISS
+#define PT_EARLY_MISS 1
+#endif
+#ifndef PT_LIT_MAX
+#define PT_LIT_MAX 0.0  // literal-step hint after a prefix stops short (measured slower on the GPU: off)
+#endif
 #ifndef PT_BLOCK_SCALE
 #define PT_BLOCK_SCALE 1.25
 #endif
@@ -488,6 +529,9 @@ struct MarchState {
     int64_t lim;  // steps_in_range from the current point for this pass (-1: not known yet)
     int pass, passes;
     uint32_t iters;  // guard: a march that has not ended after MARCH_GUARD iterations is dropped
+    int adv;         // 1 while a proven block's exact advance is still walking binade segments
+    int lit;         // literal steps to take before the next proof attempt (the crossing is near)
+    double na[4];    // steps still to apply to t, px, py, pz during an advance
 };
 enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2 };
 constexpr uint32_t MARCH_GUARD = 1u << 24;
@@ -513,13 +557,32 @@ PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz
     m->passes = passes;
     m->lim = -1;
     m->iters = 0;
+    m->adv = 0;
+    m->lit = 0;
     return true;
+}
+
+// One round of a proven block's exact advance: one binade segment for each
+// of t, px, py, pz that still has steps to go; when all are done the block's
+// end point is exact and f is evaluated there.
+PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
+    PT_MHOOK(block_begin);
+    for (int round = 0; round < PT_ADV_ROUNDS; round++) {
+        if (m.na[0] > 0.0) seg_step(m.t, m.s, m.na[0]);
+        if (m.na[1] > 0.0) seg_step(m.px, cx, m.na[1]);
+        if (m.na[2] > 0.0) seg_step(m.py, cy, m.na[2]);
+        if (m.na[3] > 0.0) seg_step(m.pz, cz, m.na[3]);
+        if (!(m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0)) break;
+    }
+    if (m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0) return;
+    m.adv = 0;
+    m.r = heart_f(m.px, m.py, m.pz);
 }
 
 // One iteration of the march loop: a proven jump, or one literal step (after a
 // failed proof).  M_DONE: the passes ended (the caller applies the final
 // t-in-[min_t, max_t] test); M_MISS: t left [start, end].
-template <bool STATS>
+template <bool STATS, bool INLINE_ADV = true>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
     PT_MPROF(iters);
     if (m.pass >= m.passes) return M_DONE;
@@ -527,9 +590,17 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
     // 2^24 of them is one the reference itself would not finish (a step below
     // t's rounding, say).  Dropping it keeps every GPU wave finite.
     if (++m.iters > MARCH_GUARD) return M_MISS;
-    if (m.t > m.end || m.t < m.start) return M_MISS;
     double s = m.s;
     double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
+    if (m.adv) {
+        march_advance(m, cx, cy, cz);
+        return M_RUNNING;
+    }
+    if (m.t > m.end || m.t < m.start) return M_MISS;
+    if (m.lit > 0) {
+        m.lit--;
+        goto literal;
+    }
     // ---- try to jump a block of b steps (exact advance + sign proof)
     if (m.r != 0.0) {
         // the range limit moves with the sequence: computed once per pass
@@ -545,19 +616,35 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             const double sgn = m.r > 0.0 ? 1.0 : -1.0;
             const double guess = poly_root_guess(P, sgn, (double)bmax);
             if (guess < PT_MIN_GUESS) goto literal;  // the crossing is the next step or two
-            int64_t B = (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
-            B = B > bmax ? bmax : (B < 2 ? 2 : B);
-            const int64_t good = poly_prefix(P, B, sgn);
+            // No crossing predicted before the range end: try to prove every
+            // step up to (an upper bound on) the one that leaves the range;
+            // then nothing can stop this pass first and the march misses.
+            const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
+            int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
+            if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
+            int64_t good = poly_prefix(P, B, sgn);
+            if (ub < BIG && good >= ub) return M_MISS;
+            good = good > bmax ? bmax : good;
             if (good >= 2) {
-                PT_MHOOK(block_begin);
-                m.t = advance(m.t, s, good);
-                m.px = advance(m.px, cx, good);
-                m.py = advance(m.py, cy, good);
-                m.pz = advance(m.pz, cz, good);
-                PT_MHOOK(block_end);
-                m.r = heart_f(m.px, m.py, m.pz);
+                // the block's exact advance runs one binade segment per
+                // coordinate per iteration (march_advance), so a lane whose
+                // coordinates cross many binades does not stall its wave
+                m.na[0] = m.na[1] = m.na[2] = m.na[3] = (double)good;
                 m.lim -= good;
+                m.adv = 1;
+                if (PT_LIT_MAX > 0.0 && good < B) m.lit = (int)fmin(PT_LIT_MAX, fmax(1.0, ceil(guess - (double)good)));
                 if (STATS) st->blocks++;
+                if (INLINE_ADV) {
+                    // one loop per coordinate: a lane pays only for the binade
+                    // segments each coordinate actually crosses
+                    m.t = advance(m.t, s, good);
+                    m.px = advance(m.px, cx, good);
+                    m.py = advance(m.py, cy, good);
+                    m.pz = advance(m.pz, cz, good);
+                    m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
+                    m.adv = 0;
+                    m.r = heart_f(m.px, m.py, m.pz);
+                }
                 return M_RUNNING;
             }
         }
@@ -579,11 +666,26 @@ literal:
         m.s = s * -0.01;
         m.r = next;
         m.lim = -1;
+        m.lit = 0;
         m.pass++;
         return m.pass >= m.passes ? M_DONE : M_RUNNING;
     }
     m.r = next;
     return M_RUNNING;
+}
+
+// What the next march_iter call will do, for wave-level phase scheduling
+// (wf_march): MP_CHEAP = a literal step or the end of the march, MP_ADV = an
+// advance round of a proven block, MP_PROOF = build the polynomial and prove
+// a block (which may still end in a literal step).  Computes the pass's range
+// limit if it is not known yet, exactly as march_iter would.
+enum MarchPhase : int { MP_CHEAP = 0, MP_ADV = 1, MP_PROOF = 2 };
+PT_HD int march_phase(MarchState &m) {
+    if (m.pass >= m.passes || m.iters + 1 > MARCH_GUARD) return MP_CHEAP;
+    if (m.adv) return MP_ADV;
+    if (m.t > m.end || m.t < m.start || m.lit > 0 || m.r == 0.0) return MP_CHEAP;
+    if (m.lim < 0) m.lim = steps_in_range_lb(m.t, m.s, m.start, m.end, (int64_t)1 << 24);
+    return m.lim >= 2 ? MP_PROOF : MP_CHEAP;
 }
 
 // RayMarchingShape::ray_intersect for the Heart in object space (o, d):

@@ -177,17 +177,38 @@ struct StatusHas {
 };
 
 // Marches of iteration `it`.  Each workgroup owns a contiguous slice of the
-// march queue and hands jobs to its lanes through an LDS counter; every lane
-// keeps its next job's ray already loaded (the index one job further ahead)
-// so a lane that finishes starts the next march without waiting on memory.
-// A job is trace_pixel's SELECT/MARCH loop over the marched shapes for one
-// path; (best, who) go back to the path, which the next bounce kernel reads
-// straight from this queue.
+// (id-sorted) march queue and hands jobs to its lanes through an LDS counter;
+// the marched shapes' select data (padded box, inverse transform, step,
+// passes) is staged in LDS once per workgroup.  A job is trace_pixel's
+// SELECT/MARCH loop over the marched shapes for one path; (best, who) go back
+// to the path, which the next bounce kernel reads from the live list.
+#ifndef PT_WF_VOTE
+#define PT_WF_VOTE 0
+#endif
+#ifndef PT_WF_PREFETCH
+#define PT_WF_PREFETCH 0
+#endif
+#ifndef PT_WF_SEL_BATCH
+#define PT_WF_SEL_BATCH 0
+#endif
+#ifndef PT_WF_MARCH_WAVES
+#define PT_WF_MARCH_WAVES 5  // waves per SIMD the march kernel's registers must allow
+#endif
+#ifndef PT_WF_LDS_SHAPES
+#define PT_WF_LDS_SHAPES 0  // marched shapes staged in LDS (measured slower than the L2-cached scene: off)
+#endif
+constexpr int WF_MAXM = PT_WF_LDS_SHAPES > 0 ? PT_WF_LDS_SHAPES : 1;  // marched shapes staged in LDS
+
 struct MarchJob {
     uint32_t id;
     Ray ray;
     double best;
     int who;
+};
+
+struct LdsShape {
+    double lo[3], hi[3], inv[12], step;
+    int depth, index;
 };
 
 __device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob *j) {
@@ -198,33 +219,101 @@ __device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob 
     j->who = v.who[id];
 }
 
-__global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it) {
+// DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
+// 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
+// s_memtime cycles, summed per wave into diag[0..35] (tuning only).
+template <bool DIAG>
+__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag) {
     __shared__ uint32_t head;
+    __shared__ LdsShape msh[WF_MAXM];
+    const int nm = sc.nmarch;
+    const int nms = PT_WF_LDS_SHAPES == 0 ? 0 : (nm < WF_MAXM ? nm : WF_MAXM);
+    for (int k = threadIdx.x; k < nms * 24; k += blockDim.x) {
+        const int i = k / 24, f = k % 24, s = sc.march[i];
+        double val;
+        if (f < 3) val = sc.boxes[s].lo[f];
+        else if (f < 6) val = sc.boxes[s].hi[f - 3];
+        else if (f < 18) val = sc.shapes[s].inv[f - 6];
+        else val = sc.shapes[s].p[0];
+        double *dst = f < 3 ? &msh[i].lo[f] : f < 6 ? &msh[i].hi[f - 3] : f < 18 ? &msh[i].inv[f - 6] : &msh[i].step;
+        if (f < 19) *dst = val;
+        if (f == 19) {
+            msh[i].depth = sc.shapes[s].depth;
+            msh[i].index = s;
+        }
+    }
     const uint32_t count = v.cnt[it * 4 + 1];
     const uint32_t *mq = v.mq;
     const uint32_t per = (count + gridDim.x - 1) / gridDim.x;
     const uint32_t lo = blockIdx.x * per, hi = min(count, lo + per);
     if (threadIdx.x == 0) head = lo + blockDim.x;
     __syncthreads();
-    // current job (slot lo + thread), next job (state in flight), index after next
     uint32_t q = lo + threadIdx.x;
     bool have = q < hi;
-    MarchJob cur, nxt;
+    MarchJob cur;
     if (have) load_job(v, mq[q], &cur);
+#if PT_WF_PREFETCH
+    // next job's state in flight, the index after it
+    MarchJob nxt;
     uint32_t qn = have ? atomicAdd(&head, 1u) : hi;
     bool nhave = qn < hi;
     if (nhave) load_job(v, mq[qn], &nxt);
     uint32_t q2 = nhave ? atomicAdd(&head, 1u) : hi;
     uint32_t id2 = q2 < hi ? mq[q2] : 0u;
+#endif
     bool marching = false;
     int km = 0, mshape = -1;
     V3 inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchState ms;
     march::MarchStats mst{0, 0, 0};
-    while (have) {
+    unsigned long long dtrips[16], dcyc[16], dlanes[4];
+    if (DIAG) {
+        for (int k = 0; k < 16; k++) dtrips[k] = dcyc[k] = 0;
+        for (int k = 0; k < 4; k++) dlanes[k] = 0;
+    }
+    unsigned long long t_prev = DIAG ? __builtin_amdgcn_s_memtime() : 0;
+    int mask_prev = -1;
+    while (DIAG ? __ballot(have) != 0 : have) {
+        if (DIAG) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            if (mask_prev >= 0) {
+                dtrips[mask_prev]++;
+                dcyc[mask_prev] += now - t_prev;
+            }
+            t_prev = now;
+            const int phd = !have ? -1 : (marching ? march::march_phase(ms) : 3);
+            const int kind = phd < 0 ? -1 : (phd == 3 ? 1 : (phd == march::MP_CHEAP ? 0 : (phd == march::MP_ADV ? 2 : 3)));
+            int mk = 0;
+            for (int k = 0; k < 4; k++) {
+                const uint64_t b = __ballot(kind == k);
+                if (b) mk |= 1 << k;
+                dlanes[k] += __popcll(b);
+            }
+            mask_prev = mk;
+        }
+        if (!have) continue;
+#if PT_WF_SEL_BATCH
+        // Job ends/switches load the next job's ray from HBM, a wait the
+        // whole wave pays: lanes needing one wait until >= PT_WF_SEL_BATCH of
+        // them do (or nothing else runs), so one wait serves many lanes.
+        {
+            const bool want_sel = !marching;
+            const uint64_t msel = __ballot(want_sel);
+            if (want_sel && __popcll(msel) < PT_WF_SEL_BATCH && msel != __ballot(true)) continue;
+        }
+#endif
+#if PT_WF_VOTE
+        // Phase vote: the wave runs one kind of work per trip, cheapest
+        // first; the proof runs only when every live lane waits for it.
+        const int ph = marching ? march::march_phase(ms) : 3;
+        const uint64_t m_cheap = __ballot(ph == march::MP_CHEAP), m_sel = __ballot(ph == 3),
+                       m_adv = __ballot(ph == march::MP_ADV);
+        const int run = m_cheap ? march::MP_CHEAP : (m_sel ? 3 : (m_adv ? march::MP_ADV : march::MP_PROOF));
+        if (ph != run) continue;
+#endif
         bool done = false;
         if (marching) {
-            const int st = march::march_iter<false>(ms, &mst);
+            const int st = march::march_iter<false, PT_WF_VOTE == 0>(ms, &mst);
             if (st != march::M_RUNNING) {
                 // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                 if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
@@ -236,16 +325,28 @@ __global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it)
             }
         } else {
             // select: next marched shape whose bound is entered before `best`
-            while (km < sc.nmarch) {
-                const int s = sc.march[km++];
-                const DBox &b = sc.boxes[s];
-                if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                const DShape &S = sc.shapes[s];
-                const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                    mshape = s;
-                    marching = true;
-                    break;
+            while (km < nm) {
+                const int k = km++;
+                if (k < nms) {
+                    const LdsShape &S = msh[k];
+                    if (!dev::slab(S.lo, S.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                    const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                    if (march::march_begin(S.step, S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                        mshape = S.index;
+                        marching = true;
+                        break;
+                    }
+                } else {
+                    const int s = sc.march[k];
+                    const DBox &b = sc.boxes[s];
+                    if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                    const DShape &S = sc.shapes[s];
+                    const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                    if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                        mshape = s;
+                        marching = true;
+                        break;
+                    }
                 }
             }
             done = !marching;
@@ -253,17 +354,37 @@ __global__ __launch_bounds__(256) void wf_march(dev::Scene sc, WfView v, int it)
         if (done) {
             v.t[cur.id] = cur.best;
             v.who[cur.id] = cur.who;
+#if PT_WF_PREFETCH
             have = nhave;
             if (have) {
                 cur = nxt;
-                inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
-                km = 0;
                 nhave = q2 < hi;
                 if (nhave) load_job(v, id2, &nxt);
                 q2 = nhave ? atomicAdd(&head, 1u) : hi;
                 id2 = q2 < hi ? mq[q2] : 0u;
             }
+#else
+            q = atomicAdd(&head, 1u);
+            have = q < hi;
+            if (have) load_job(v, mq[q], &cur);
+#endif
+            if (have) {
+                inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
+                km = 0;
+            }
         }
+    }
+    if (DIAG && (threadIdx.x & 63) == 0) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        if (mask_prev >= 0) {
+            dtrips[mask_prev]++;
+            dcyc[mask_prev] += now - t_prev;
+        }
+        for (int k = 0; k < 16; k++) {
+            atomicAdd(&diag[k], dtrips[k]);
+            atomicAdd(&diag[16 + k], dcyc[k]);
+        }
+        for (int k = 0; k < 4; k++) atomicAdd(&diag[32 + k], dlanes[k]);
     }
 }
 
@@ -319,6 +440,8 @@ static uint32_t wf_cap_paths() {
 }
 
 void wave_workspace_free(WaveWorkspace *ws) {
+    if (ws->diag) (void)hipFree(ws->diag);
+    ws->diag = nullptr;
     if (ws->base) (void)hipFree(ws->base);
     ws->base = nullptr;
     ws->bytes = 0;
@@ -413,7 +536,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
         }
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march, 256, 0) == hipSuccess && occ > 0) per = occ;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march<false>, 256, 0) == hipSuccess && occ > 0)
+            per = occ;
         const char *e = getenv("PT_WF_MARCH_BLOCKS_PER_CU");  // tuning knob
         if (e && atoi(e) > 0 && atoi(e) < per) per = atoi(e);
         return (uint32_t)(cus * per);
@@ -449,7 +573,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.mq,
                                              &v.cnt[it * 4 + 1], (int64_t)paths, StatusHas{v.status, 2}, st);
                 if (e != hipSuccess) return e;
-                wf_march<<<march_blocks, 256, 0, st>>>(sc, v, it);
+                if (ws->diag) wf_march<true><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);
+                else wf_march<false><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             wf_reduce<<<(v.npix + 255) / 256, 256, 0, st>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);

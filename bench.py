@@ -25,10 +25,12 @@ METRIC = "Msamples/sec cornell_box 1920x1080x256spp at 1/2/4/8 MI355X; RMS pixel
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (FMA = 2 FLOP); no-FMA instruction peak is half of it
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
 
-# FLOPs per event of the kernel's own traversal (counted in pt_device.hpp /
+# FLOPs per event of the kernels' own traversal (counted in pt_device.hpp /
 # pt_march.hpp; f64 add/sub/mul/div/sqrt = 1 FLOP, compares, min/max and
 # integer ops not counted).  Event counts come from the GPU itself
-# (pt_count_work, a diagnostic build of the same kernel) on a pixel sample.
+# (pt_count_work, a diagnostic build of the same device functions) on a pixel
+# sample.  The march events run in the wavefront engine's march kernel, the
+# rest in its bounce kernel.
 FLOP_WEIGHTS = {
     "samples": 31,        # jittered camera ray + normalize (28), accumulate (3)
     "bounces": 11,        # reciprocal direction (3), background on a miss (8)
@@ -36,16 +38,19 @@ FLOP_WEIGHTS = {
     "test_rect": 37, "test_cube": 45,
     "test_march": 64,     # transform (33) + bounding-ellipsoid quadratic (31)
     "node_slabs": 12, "march_slabs": 12,
-    "march_steps": 19,    # t, p accumulation (4) + heart_f (15)
-    "march_tries": 45,    # interval bound of heart_f over a block's box
-    "march_blocks": 15,   # heart_f at the block end
+    "march_steps": 19,    # literal step: t, p adds (4) + heart_f (15)
+    "march_tries": 400,   # degree-6 expansion (140), root guess (20), Bernstein prefix
+                          # setup + margin (95), ~3 de Casteljau halvings (145)
+    "march_blocks": 135,  # exact advance of t, p over ~2.5 binade segments each + heart_f
     "hits": 100,          # object point/normal, normalisations, world transforms
     "lambert": 20, "metal": 25, "dielectric": 40, "reject_tries": 14, "unwind": 3,
 }
+MARCH_EVENTS = ("test_march", "march_slabs", "march_steps", "march_tries", "march_blocks")
 
 
-def flops_per_sample(cnt):
-    return sum(FLOP_WEIGHTS[k] * cnt[k] for k in FLOP_WEIGHTS) / max(1, cnt["samples"])
+def flops_per_sample(cnt, keys=None):
+    keys = FLOP_WEIGHTS if keys is None else keys
+    return sum(FLOP_WEIGHTS[k] * cnt[k] for k in keys) / max(1, cnt["samples"])
 
 
 def parse():
@@ -155,6 +160,7 @@ def main():
     torch.cuda.synchronize()
     k_start.clear()
     k_end.clear()
+    pt.kernel_timing(r, True)  # per-kernel HIP events on the launch stream, timed steps only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -165,6 +171,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kt = pt.kernel_timing(r, False)
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
@@ -180,11 +187,16 @@ def main():
         sys.path.insert(0, str(ROOT / "oracle"))
         threads = min(16, os.cpu_count() or 1)
 
-        # roofline of the dominant kernel (render_tiles), this rank's launches
+        # roofline of the dominant kernel, this rank's launches in the timed steps
         F, counts = algorithmic_flops(pt, r, cam, args)
         my_tiles = pt.shard_tiles(W, H, rank, world)
-        samples_launch = samples_frame * my_tiles / (pt.shard_tiles(W, H, 0, 1))
-        achieved = F * samples_launch / (kernel_ms / 1e3) / 1e12
+        samples_rank = samples_frame * my_tiles / (pt.shard_tiles(W, H, 0, 1)) * args.steps
+        f_kind = {"march": flops_per_sample(counts, MARCH_EVENTS),
+                  "bounce": flops_per_sample(counts, [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS]),
+                  "megakernel": F}
+        dom = max(("bounce", "march", "megakernel"), key=lambda k: kt[k][0])
+        dom_ms, dom_n = kt[dom]
+        achieved = f_kind[dom] * samples_rank / (dom_ms / 1e3) / 1e12
         out_bytes = 24.0 * W * H * my_tiles / pt.shard_tiles(W, H, 0, 1)
         rec = {
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
@@ -194,11 +206,16 @@ def main():
             "config": {"workload": "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth),
                        "width": W, "height": H, "spp": spp, "depth": args.depth, "seed": args.seed,
                        "parallelism": "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"},
-            "roofline": {"bound": "valu_f64", "achieved": round(achieved, 3), "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4), "traffic": None,
-                         "flops_per_sample": round(F, 1), "kernel": "render_tiles", "events_per_sample":
-                             {k: round(v / max(1, counts["samples"]), 3) for k, v in counts.items() if k != "samples"},
-                         "kernel_ms_avg": round(kernel_ms, 3), "kernel_ms_max_rank": round(kernel_ms_max, 3)},
+            "roofline": {"bound": "valu_f64", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
+                         "kernel": "wf_" + dom if dom != "megakernel" else "render_tiles",
+                         "flops_per_sample": round(f_kind[dom], 1), "launches": dom_n,
+                         "kernel_ms_avg": round(dom_ms / max(1, dom_n), 4),
+                         "kernel_ms_by_kind": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+                         "flops_per_sample_total": round(F, 1),
+                         "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
+                                               for k, v in counts.items() if k != "samples"},
+                         "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3)},
             "roofline_hbm": {"achieved": round(out_bytes / (kernel_ms / 1e3) / 1e9, 4), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},

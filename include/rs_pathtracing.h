@@ -166,6 +166,15 @@ int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint3
  * Diagnostic / parity probe. */
 int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters);
 
+/* Per-kernel launch timing of the render path (bench / roofline): returns
+ * the summed HIP-event durations (ms) and launch counts per kernel kind since
+ * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
+ * reduce, [4] megakernel — into ms[nkinds] / launches[nkinds] (either may be
+ * NULL), then turns recording on (enable = 1) or off.  Events are recorded on
+ * the stream each kernel is launched on. */
+#define PT_KERNEL_KINDS 5
+int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
+
 /* Diagnostic of the wavefront march kernel: returns (and clears) the counters
  * accumulated since the last call into out[min(n, 36)] — trips and s_memtime
  * cycles per mix of lane phases (16 + 16), lanes per phase (4) — and turns

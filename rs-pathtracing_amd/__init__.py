@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
     "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
     "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_wave_diag", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_wave_diag", "pt_kernel_timing", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -133,6 +133,7 @@ def lib():
                                     C.POINTER(u64)]),
         "pt_march_jobs": (C.c_int, [vp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                     C.POINTER(C.c_uint32)]),
+        "pt_kernel_timing": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(u32), sz]),
         "pt_wave_diag": (C.c_int, [vp, C.c_int, C.POINTER(u64), sz]),
         "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
@@ -356,6 +357,18 @@ def march_jobs(renderer: "HipRenderer", jobs):
     _check(lib().pt_march_jobs(renderer._h, jobs.ctypes.data_as(dp), n, t.ctypes.data_as(dp),
                                st.ctypes.data_as(C.POINTER(C.c_int32)), it.ctypes.data_as(C.POINTER(C.c_uint32))))
     return t, st.astype(bool), it
+
+
+KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel"]
+
+
+def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
+    """Summed HIP-event time (ms) and launches per render-path kernel since the
+    last call (pt_kernel_timing); enable/disable recording for what follows."""
+    ms = (C.c_double * len(KERNEL_KINDS))()
+    n = (C.c_uint32 * len(KERNEL_KINDS))()
+    _check(lib().pt_kernel_timing(renderer._h, 1 if enable else 0, ms, n, len(KERNEL_KINDS)))
+    return {k: (ms[i], n[i]) for i, k in enumerate(KERNEL_KINDS)}
 
 
 def wave_diag(renderer: "HipRenderer", enable: bool = True):

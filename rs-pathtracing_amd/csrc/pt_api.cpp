@@ -453,6 +453,24 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
     return PT_OK;
 }
 
+int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds) {
+    if (!r) return fail(PT_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(r->device));
+    double m[K_KINDS];
+    uint32_t l[K_KINDS];
+    HIP_TRY(timer_collect(r->ws.timer, m, l));
+    for (size_t k = 0; k < nkinds && k < (size_t)K_KINDS; k++) {
+        if (ms) ms[k] = m[k];
+        if (launches) launches[k] = l[k];
+    }
+    if (enable && !r->ws.timer) r->ws.timer = timer_new();
+    if (!enable && r->ws.timer) {
+        timer_free(r->ws.timer);
+        r->ws.timer = nullptr;
+    }
+    return PT_OK;
+}
+
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(r->device));

@@ -253,6 +253,9 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
                          WaveWorkspace *ws) {
     if (P.tile_count == 0) return hipSuccess;
     if (use_wavefront(s, ws)) return launch_render_wave(dscene(s), P, out, st, ws);
+    KernelTimer *tm = ws ? ws->timer : nullptr;
+    hipError_t e0 = timer_begin(tm, st, K_MEGA);
+    if (e0 != hipSuccess) return e0;
     if (P.depth <= 8) {
         switch (render_waves()) {
         case 2: render_tiles<4, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
@@ -262,7 +265,9 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
     } else {
         PT_DISPATCH_NW(P.depth, (render_tiles<NW, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out)));
     }
-    return hipGetLastError();
+    e0 = hipGetLastError();
+    if (e0 != hipSuccess) return e0;
+    return timer_end(tm, st);
 }
 
 hipError_t launch_unshard(const double *g, uint32_t width, uint32_t height, uint32_t world, double *frame,

@@ -18,10 +18,21 @@ struct DeviceScene {
 
 // Device workspace of the wavefront engine (pt_wave.hip), grown on demand and
 // reused by every frame of a renderer.
+// Per-kernel launch timing (pt_kernel_timing): HIP events recorded on the
+// launch stream around every render-path kernel while enabled.
+enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_KINDS = 5 };
+struct KernelTimer;
+KernelTimer *timer_new();
+void timer_free(KernelTimer *t);
+hipError_t timer_begin(KernelTimer *t, hipStream_t st, int kind);  // no-op when t is null
+hipError_t timer_end(KernelTimer *t, hipStream_t st);
+hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches);  // sums since last collect
+
 struct WaveWorkspace {
     void *base = nullptr;
     size_t bytes = 0;
     unsigned long long *diag = nullptr;  // march-kernel phase diagnostics (pt_wave_diag), when enabled
+    KernelTimer *timer = nullptr;         // per-kernel timing (pt_kernel_timing), when enabled
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

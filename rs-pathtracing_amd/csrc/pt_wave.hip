@@ -35,6 +35,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
+#include <vector>
 
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
@@ -421,6 +422,58 @@ __global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int fi
     }
 }
 
+// ------------------------------------------------------------- kernel timer
+struct KernelTimer {
+    struct Rec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    hipEvent_t get() {
+        if (used == pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            pool.push_back(e);
+        }
+        return pool[used++];
+    }
+};
+KernelTimer *timer_new() { return new KernelTimer; }
+void timer_free(KernelTimer *t) {
+    if (!t) return;
+    for (auto e : t->pool) (void)hipEventDestroy(e);
+    delete t;
+}
+hipError_t timer_begin(KernelTimer *t, hipStream_t st, int kind) {
+    if (!t) return hipSuccess;
+    KernelTimer::Rec r{kind, t->get(), t->get()};
+    if (!r.a || !r.b) return hipErrorOutOfMemory;
+    t->recs.push_back(r);
+    return hipEventRecord(r.a, st);
+}
+hipError_t timer_end(KernelTimer *t, hipStream_t st) {
+    if (!t || t->recs.empty()) return hipSuccess;
+    return hipEventRecord(t->recs.back().b, st);
+}
+hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches) {
+    for (int k = 0; k < K_KINDS; k++) ms[k] = 0.0, launches[k] = 0;
+    if (!t) return hipSuccess;
+    for (auto &r : t->recs) {
+        hipError_t e = hipEventSynchronize(r.b);
+        if (e != hipSuccess) return e;
+        float x = 0.f;
+        e = hipEventElapsedTime(&x, r.a, r.b);
+        if (e != hipSuccess) return e;
+        ms[r.kind] += x;
+        launches[r.kind]++;
+    }
+    t->recs.clear();
+    t->used = 0;
+    return hipSuccess;
+}
+
 // ------------------------------------------------------------- host driver
 static size_t path_bytes(int nw) { return 7 * 8 + 8 + 4 + 4 + (size_t)nw * 8 + 3 * 8 + 2 * 4 + 1; }
 
@@ -440,6 +493,8 @@ static uint32_t wf_cap_paths() {
 }
 
 void wave_workspace_free(WaveWorkspace *ws) {
+    timer_free(ws->timer);
+    ws->timer = nullptr;
     if (ws->diag) (void)hipFree(ws->diag);
     ws->diag = nullptr;
     if (ws->base) (void)hipFree(ws->base);
@@ -556,15 +611,20 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             uint32_t bb = (paths + 255) / 256;
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
+            if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
             launch_bounce<NW, true>((paths + 255) / 256, st, sc, P0, v, 0);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
+                    if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
                     launch_bounce<NW, false>(bb, st, sc, P0, v, it);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
+                    if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
                 }
                 if (it == iters - 1) break;  // the last bounce only shades
                 // live list for it + 1 and march queue for it, both id-sorted
+                if ((e = timer_begin(ws->timer, st, K_SELECT)) != hipSuccess) return e;
                 size_t tb = sel_bytes;
                 e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.list,
                                              &v.cnt[(it + 1) * 4 + 0], (int64_t)paths, StatusHas{v.status, 1}, st);
@@ -573,12 +633,17 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.mq,
                                              &v.cnt[it * 4 + 1], (int64_t)paths, StatusHas{v.status, 2}, st);
                 if (e != hipSuccess) return e;
+                if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
+                if ((e = timer_begin(ws->timer, st, K_MARCH)) != hipSuccess) return e;
                 if (ws->diag) wf_march<true><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);
                 else wf_march<false><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
             }
+            if ((e = timer_begin(ws->timer, st, K_REDUCE)) != hipSuccess) return e;
             wf_reduce<<<(v.npix + 255) / 256, 256, 0, st>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
         }
     }
     return hipSuccess;

@@ -354,8 +354,10 @@ struct IdStack {
 // One bounce of ray_color (src/renderer/mod.rs:23-45).  Returns true when the
 // path ends, with the leaf radiance in *leaf; otherwise advances ray/depth.
 // Everything in a bounce after the closest hit (who, t) is known.
-template <int NW, bool STATS = false>
-PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng,
+// Stack: any type with push(id), pop() and a count n (IdStack in registers,
+// or the wavefront engine's per-slot id array in HBM).
+template <bool STATS = false, class Stack>
+PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, Stack &stk, Rng &rng,
                  double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
         *leaf = background(ray.d);
@@ -412,11 +414,11 @@ PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, 
     double t;
     if (STATS) ct->c[C_BOUNCES]++;
     int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
-    return shade<NW, STATS>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
+    return shade<STATS>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
 }
 
-template <int NW, bool STATS = false>
-PT_HD V3 unwind(const Scene &sc, IdStack<NW> &stk, V3 c, Ctr *ct = nullptr) {
+template <bool STATS = false, class Stack>
+PT_HD V3 unwind(const Scene &sc, Stack &stk, V3 c, Ctr *ct = nullptr) {
     while (stk.n > 0) {
         if (STATS) ct->c[C_UNWIND]++;
         const DMaterial &m = sc.mats[stk.pop()];
@@ -433,7 +435,7 @@ PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s1
     V3 leaf;
     while (!bounce<NW>(sc, ray, depth, stk, rng, s11, &leaf)) {
     }
-    return unwind<NW>(sc, stk, leaf);
+    return unwind(sc, stk, leaf);
 }
 
 // Camera sample: MultisamplerRayCaster::next (ray_caster.rs:103-118), u then v.
@@ -548,7 +550,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_SHADE) {
             V3 leaf;
             uint64_t tf = 0;
-            const bool ended = shade<NW, STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
+            const bool ended = shade<STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
                                                 TIMING ? &tf : nullptr);
             if (TIMING) {
                 uint64_t n = PT_STAMP();
@@ -559,7 +561,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                 ts = n;
             }
             if (ended) {
-                acc = add(acc, unwind<NW, STATS>(sc, stk, leaf, ct));
+                acc = add(acc, unwind<STATS>(sc, stk, leaf, ct));
                 if (STATS) ct->c[C_SAMPLES]++;
                 if (++s == P.spp) break;
                 rng.s = sample_key(P.seed, pixel, s);

@@ -32,8 +32,6 @@
 // bit-identical.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
-
 #include <cstdlib>
 #include <vector>
 
@@ -51,7 +49,7 @@ struct WfView {
     uint64_t *rng;
     int32_t *who;    // best hit shape (-1: miss)
     uint32_t *meta;  // depth | stack count << 8
-    uint64_t *stk;   // NW words per path, word k at stk[k * cap + id]
+    uint32_t *ids;   // attenuation-id stack: entry k of a path at ids[k * cap + id]
     double *rx, *ry, *rz;  // sample radiance of finished paths
     uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
     uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
@@ -66,6 +64,23 @@ struct WfView {
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
+
+// The attenuation-id stack of a path kept in HBM: a push writes one 32-bit
+// id (once, where the recursion would have pushed it); the ids are read back
+// only when the path ends (unwind).
+struct MemStack {
+    uint32_t *base;
+    size_t stride;
+    int n;
+    __device__ __forceinline__ void push(uint32_t id) {
+        base[(size_t)n * stride] = id;
+        n++;
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        n--;
+        return base[(size_t)n * stride];
+    }
+};
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
 // thread-in-tile laid out as render_tiles' 4 waves of 8x8.
@@ -100,8 +115,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         Ray ray;
         dev::Rng rng{0};
         uint32_t depth = 0;
-        dev::IdStack<NW> stk;
-        stk.clear();
+        MemStack stk{v.ids, (size_t)v.cap, 0};
         if (live) {
             if (FIRST) {
                 id = i;
@@ -121,12 +135,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 rng.s = v.rng[id];
                 const uint32_t meta = v.meta[id];
                 depth = meta & 0xffu;
+                stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
-#pragma unroll
-                for (int k = 0; k < NW; k++) stk.w[k] = v.stk[(size_t)k * v.cap + id];
                 V3 leaf;
-                if (dev::shade<NW>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
-                    const V3 c = dev::unwind<NW>(sc, stk, leaf);
+                if (dev::shade(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                    const V3 c = dev::unwind(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
                     v.rz[id] = c.z;
@@ -161,21 +174,109 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             v.who[id] = who;
             v.rng[id] = rng.s;
             v.meta[id] = depth | ((uint32_t)stk.n << 8);
-#pragma unroll
-            for (int k = 0; k < NW; k++) v.stk[(size_t)k * v.cap + id] = stk.w[k];
         }
         if (i < count) v.status[id] = live ? (need_march ? 3u : 1u) : 0u;
     }
 }
 
-// Order-preserving compaction of the status bytes into id lists (hipcub
-// select): neighbouring pixels stay in neighbouring lanes, so the next
-// kernels' structure-of-arrays loads stay coalesced and march waves coherent.
-struct StatusHas {
-    const uint8_t *st;
-    uint8_t bit;
-    __host__ __device__ bool operator()(const uint32_t &id) const { return (st[id] & bit) != 0; }
-};
+// Order-preserving compaction of the status bytes into the two id lists
+// (live paths: bit 0, march jobs: bit 1) in three small launches: per-tile
+// counts (16 statuses per thread, one 16-byte load), one scan over the tile
+// counts, and an ordered scatter.  Neighbouring pixels stay in neighbouring
+// lanes, so the next kernels' structure-of-arrays loads stay coalesced and
+// march waves coherent.
+constexpr int CP_ITEMS = 16, CP_BLOCK = 256, CP_TILE = CP_ITEMS * CP_BLOCK;
+
+__device__ __forceinline__ void cp_bits(uint4 q, uint32_t *live, uint32_t *march) {
+    // statuses are 0, 1 or 3: bit 0 of each byte = live, bit 1 = march
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint32_t l = 0, m = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        l += __popc(w[k] & 0x01010101u);
+        m += __popc(w[k] & 0x02020202u);
+    }
+    *live = l;
+    *march = m;
+}
+
+// block-wide exclusive scan of one value per thread (256 threads, 4 waves)
+__device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, uint32_t *lds /*4*/) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) lds[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if ((uint32_t)k < wv) before += lds[k];
+        tot += lds[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return before + inc - x;
+}
+
+__global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk) {
+    __shared__ uint32_t lds[8];
+    const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    uint32_t l, m, tl, tm;
+    cp_bits(q, &l, &m);
+    block_exscan(l, &tl, lds);
+    block_exscan(m, &tm, lds + 4);
+    if (threadIdx.x == 0) {
+        blk[2 * blockIdx.x] = tl;
+        blk[2 * blockIdx.x + 1] = tm;
+    }
+}
+
+// one block: exclusive scan of the (live, march) tile counts in place; totals
+// go to the counters the next kernels read
+__global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, uint32_t *__restrict__ n_live,
+                                               uint32_t *__restrict__ n_march) {
+    __shared__ uint32_t lds[8];
+    uint32_t cl = 0, cm = 0;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += blockDim.x) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t l = b < nblk ? blk[2 * b] : 0u, m = b < nblk ? blk[2 * b + 1] : 0u;
+        uint32_t tl, tm;
+        const uint32_t el = block_exscan(l, &tl, lds), em = block_exscan(m, &tm, lds + 4);
+        if (b < nblk) {
+            blk[2 * b] = cl + el;
+            blk[2 * b + 1] = cm + em;
+        }
+        cl += tl;
+        cm += tm;
+    }
+    if (threadIdx.x == 0) {
+        *n_live = cl;
+        *n_march = cm;
+    }
+}
+
+__global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st, const uint32_t *__restrict__ blk,
+                                                  uint32_t *__restrict__ live_out, uint32_t *__restrict__ march_out) {
+    __shared__ uint32_t lds[8];
+    const size_t base = (size_t)blockIdx.x * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
+    const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    uint32_t l, m, tl, tm;
+    cp_bits(q, &l, &m);
+    uint32_t ol = blk[2 * blockIdx.x] + block_exscan(l, &tl, lds);
+    uint32_t om = blk[2 * blockIdx.x + 1] + block_exscan(m, &tm, lds + 4);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < CP_ITEMS; k++) {
+        const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        const uint32_t id = (uint32_t)(base + k);
+        if (b & 1u) live_out[ol++] = id;
+        if (b & 2u) march_out[om++] = id;
+    }
+}
 
 // Marches of iteration `it`.  Each workgroup owns a contiguous slice of the
 // (id-sorted) march queue and hands jobs to its lanes through an LDS counter;
@@ -475,16 +576,7 @@ hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches) {
 }
 
 // ------------------------------------------------------------- host driver
-static size_t path_bytes(int nw) { return 7 * 8 + 8 + 4 + 4 + (size_t)nw * 8 + 3 * 8 + 2 * 4 + 1; }
-
-// temp storage of one select over n slots
-static size_t select_bytes(uint32_t n) {
-    size_t b = 0;
-    StatusHas pred{nullptr, 1};
-    (void)hipcub::DeviceSelect::If(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0), (uint32_t *)nullptr,
-                                   (uint32_t *)nullptr, (int64_t)n, pred, (hipStream_t)0);
-    return b;
-}
+static size_t path_bytes(uint32_t depth) { return 7 * 8 + 8 + 4 + 4 + (size_t)(depth + 1) * 4 + 3 * 8 + 2 * 4 + 1; }
 
 static uint32_t wf_cap_paths() {
     const char *e = getenv("PT_WF_PATHS");
@@ -549,8 +641,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const uint32_t cap = ns * npix_max;
     const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
     const size_t cnt_words = (size_t)(iters + 2) * 4;
-    const size_t sel_bytes = select_bytes(cap);
-    const size_t bytes = (size_t)cap * path_bytes(NW) + (size_t)npix_max * 24 + cnt_words * 4 + sel_bytes + 4096;
+    const uint32_t cap_tiles = (cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
+    const size_t bytes = (size_t)cap * path_bytes(P0.depth) + (size_t)cap_tiles * CP_TILE + (size_t)cap_tiles * 8 +
+                         (size_t)npix_max * 24 + cnt_words * 4 + 8192;
     hipError_t e = reserve(ws, bytes);
     if (e != hipSuccess) return e;
     // carve the workspace
@@ -571,14 +664,14 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     v.rng = (uint64_t *)take((size_t)cap * 8);
     v.who = (int32_t *)take((size_t)cap * 4);
     v.meta = (uint32_t *)take((size_t)cap * 4);
-    v.stk = (uint64_t *)take((size_t)cap * 8 * NW);
+    v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
     v.rx = (double *)take((size_t)cap * 8);
     v.ry = (double *)take((size_t)cap * 8);
     v.rz = (double *)take((size_t)cap * 8);
     v.list = (uint32_t *)take((size_t)cap * 4);
     v.mq = (uint32_t *)take((size_t)cap * 4);
-    v.status = (uint8_t *)take((size_t)cap);
-    void *sel_tmp = take(sel_bytes);
+    v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
+    uint32_t *cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
     v.acc = (double *)take((size_t)npix_max * 24);
     v.cnt = (uint32_t *)take(cnt_words * 4);
     if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
@@ -608,6 +701,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             const uint32_t paths = v.ns * v.npix;
             e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, st);
             if (e != hipSuccess) return e;
+            e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, st);
+            if (e != hipSuccess) return e;
             uint32_t bb = (paths + 255) / 256;
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
@@ -625,14 +720,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if (it == iters - 1) break;  // the last bounce only shades
                 // live list for it + 1 and march queue for it, both id-sorted
                 if ((e = timer_begin(ws->timer, st, K_SELECT)) != hipSuccess) return e;
-                size_t tb = sel_bytes;
-                e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.list,
-                                             &v.cnt[(it + 1) * 4 + 0], (int64_t)paths, StatusHas{v.status, 1}, st);
-                if (e != hipSuccess) return e;
-                tb = sel_bytes;
-                e = hipcub::DeviceSelect::If(sel_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), v.mq,
-                                             &v.cnt[it * 4 + 1], (int64_t)paths, StatusHas{v.status, 2}, st);
-                if (e != hipSuccess) return e;
+                const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
+                cp_count<<<ptiles, CP_BLOCK, 0, st>>>(v.status, cp_blk);
+                cp_scan<<<1, CP_BLOCK, 0, st>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1]);
+                cp_scatter<<<ptiles, CP_BLOCK, 0, st>>>(v.status, cp_blk, v.list, v.mq);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, st, K_MARCH)) != hipSuccess) return e;
                 if (ws->diag) wf_march<true><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);

@@ -381,6 +381,12 @@ PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
     return mn > margin;
 }
 
+#ifndef PT_FOLD_LIT
+#define PT_FOLD_LIT 1
+#endif
+#ifndef PT_PREFIX_RES
+#define PT_PREFIX_RES 1.0
+#endif
 // Longest provable prefix of a block: the largest integer b <= B such that
 // sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither the
 // approx_equal stop nor a sign change can fire before step b).  One Bernstein
@@ -417,7 +423,7 @@ PT_HD int64_t poly_prefix(const Poly &P, int64_t B, double sgn) {
             proven = lo + len;
             break;
         }
-        if (len * Bd < 1.0) break;  // narrower than one step: nothing more to prove here
+        if (len * Bd < PT_PREFIX_RES) break;  // resolution reached (1 = one step): stop here
         // de Casteljau at 1/2 in place: level r overwrites c[0 .. 6-r], so
         // afterwards c[i] is the level-(6-i) point i = the right half's
         // control point i; the left half's are the levels' first points.
@@ -644,6 +650,9 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
                     m.adv = 0;
                     m.r = heart_f(m.px, m.py, m.pz);
+                    // a prefix that stopped short of B ends just before the
+                    // crossing: take that literal step in this iteration
+                    if (PT_FOLD_LIT && good < B && m.lim >= 1) goto literal;
                 }
                 return M_RUNNING;
             }

@@ -293,6 +293,9 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_SEL_BATCH
 #define PT_WF_SEL_BATCH 0
 #endif
+#ifndef PT_WF_UNITS
+#define PT_WF_UNITS 1
+#endif
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 5  // waves per SIMD the march kernel's registers must allow
 #endif
@@ -413,66 +416,70 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         const int run = m_cheap ? march::MP_CHEAP : (m_sel ? 3 : (m_adv ? march::MP_ADV : march::MP_PROOF));
         if (ph != run) continue;
 #endif
-        bool done = false;
-        if (marching) {
-            const int st = march::march_iter<false, PT_WF_VOTE == 0>(ms, &mst);
-            if (st != march::M_RUNNING) {
-                // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
-                if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
-                    (ms.t < cur.best || mshape > cur.who)) {
-                    cur.best = ms.t;
-                    cur.who = mshape;
-                }
-                marching = false;
-            }
-        } else {
-            // select: next marched shape whose bound is entered before `best`
-            while (km < nm) {
-                const int k = km++;
-                if (k < nms) {
-                    const LdsShape &S = msh[k];
-                    if (!dev::slab(S.lo, S.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                    const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                    if (march::march_begin(S.step, S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                        mshape = S.index;
-                        marching = true;
-                        break;
+        // up to PT_WF_UNITS units of work per trip (a march iteration, a
+        // select step, a job switch): short jobs do not pay a trip per step
+        for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
+            bool done = false;
+            if (marching) {
+                const int st = march::march_iter<false, PT_WF_VOTE == 0>(ms, &mst);
+                if (st != march::M_RUNNING) {
+                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
+                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
+                        (ms.t < cur.best || mshape > cur.who)) {
+                        cur.best = ms.t;
+                        cur.who = mshape;
                     }
-                } else {
-                    const int s = sc.march[k];
-                    const DBox &b = sc.boxes[s];
-                    if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                    const DShape &S = sc.shapes[s];
-                    const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                    if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                        mshape = s;
-                        marching = true;
-                        break;
+                    marching = false;
+                }
+            } else {
+                // select: next marched shape whose bound is entered before `best`
+                while (km < nm) {
+                    const int k = km++;
+                    if (k < nms) {
+                        const LdsShape &S = msh[k];
+                        if (!dev::slab(S.lo, S.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                        const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                        if (march::march_begin(S.step, S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                            mshape = S.index;
+                            marching = true;
+                            break;
+                        }
+                    } else {
+                        const int s = sc.march[k];
+                        const DBox &b = sc.boxes[s];
+                        if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                        const DShape &S = sc.shapes[s];
+                        const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                        if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                            mshape = s;
+                            marching = true;
+                            break;
+                        }
                     }
                 }
+                done = !marching;
             }
-            done = !marching;
-        }
-        if (done) {
-            v.t[cur.id] = cur.best;
-            v.who[cur.id] = cur.who;
+            if (done) {
+                v.t[cur.id] = cur.best;
+                v.who[cur.id] = cur.who;
 #if PT_WF_PREFETCH
-            have = nhave;
-            if (have) {
-                cur = nxt;
-                nhave = q2 < hi;
-                if (nhave) load_job(v, id2, &nxt);
-                q2 = nhave ? atomicAdd(&head, 1u) : hi;
-                id2 = q2 < hi ? mq[q2] : 0u;
-            }
+                have = nhave;
+                if (have) {
+                    cur = nxt;
+                    nhave = q2 < hi;
+                    if (nhave) load_job(v, id2, &nxt);
+                    q2 = nhave ? atomicAdd(&head, 1u) : hi;
+                    id2 = q2 < hi ? mq[q2] : 0u;
+                }
 #else
-            q = atomicAdd(&head, 1u);
-            have = q < hi;
-            if (have) load_job(v, mq[q], &cur);
+                q = atomicAdd(&head, 1u);
+                have = q < hi;
+                if (have) load_job(v, mq[q], &cur);
 #endif
-            if (have) {
-                inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
-                km = 0;
+                if (have) {
+                    inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
+                    km = 0;
+                }
             }
         }
     }

@@ -36,7 +36,12 @@ extern "C" {
 #define PT_RECTANGLE 1 /* src/world/shapes/mod.rs:150-221 */
 #define PT_CUBE 2      /* src/world/shapes/mod.rs:223-302 */
 #define PT_MARCH 3     /* RayMarchingShape, src/world/shapes/ray_marching.rs:10-110 */
-#define PT_FUNC_HEART 0
+#define PT_FUNC_HEART 0 /* ShapeFunctions, ray_marching.rs:121-520 */
+#define PT_FUNC_SINE 1
+#define PT_FUNC_STAR 2
+#define PT_FUNC_DUPIN_CYCLIDE 3
+#define PT_FUNC_HUNTS_SURFACE 4
+#define PT_FUNC_CUSHION 5
 
 /* material kinds (src/world/material.rs) */
 #define PT_LAMBERTIAN 0
@@ -68,6 +73,7 @@ typedef struct {
     int32_t type, material, inverse_normal, depth, func, pad0;
     double direct[16], inverse[16];
     double x0, y0, x1, y1, step;
+    double a, b, c, d, sphere_radius; /* ray-marched function parameters (JSON) */
 } pt_shape_info;
 
 typedef struct {
@@ -176,8 +182,9 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
 
 /* Diagnostic of the wavefront march kernel: returns (and clears) the counters
- * accumulated since the last call into out[min(n, 36)] — trips and s_memtime
- * cycles per mix of lane phases (16 + 16), lanes per phase (4) — and turns
+ * accumulated since the last call into out[min(n, 40)] — trips and s_memtime
+ * cycles per mix of lane phases (16 + 16), lanes per phase (4), then the
+ * bounce kernel's cycles per section (load+shade, trace, pre-check, store) — and turns
  * the instrumented build on (enable = 1) or off. */
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
 

@@ -22,7 +22,9 @@ HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "liboracle.so"
 
 SPHERE, RECT, CUBE, MARCH = 0, 1, 2, 3
-FUNC_HEART = 0
+FUNC_HEART, FUNC_SINE, FUNC_STAR, FUNC_DUPIN, FUNC_HUNTS, FUNC_CUSHION = 0, 1, 2, 3, 4, 5
+FUNC_IDS = {"Heart": FUNC_HEART, "Sine": FUNC_SINE, "Star": FUNC_STAR, "DupinCyclide": FUNC_DUPIN,
+            "HuntsSurface": FUNC_HUNTS, "Cushion": FUNC_CUSHION}
 LAMBERTIAN, METAL, DIELECTRIC, DIFFUSE_LIGHT, EMPTY = 0, 1, 2, 3, 4
 
 
@@ -31,7 +33,8 @@ class ShapeIn(C.Structure):
                 ("depth", C.c_int32), ("func", C.c_int32), ("pad0", C.c_int32),
                 ("translate", C.c_double * 3), ("rotate", C.c_double * 3), ("scale", C.c_double * 3),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
-                ("step", C.c_double)]
+                ("step", C.c_double), ("fa", C.c_double), ("fb", C.c_double), ("fc", C.c_double),
+                ("fd", C.c_double), ("fr", C.c_double)]
 
 
 class MaterialIn(C.Structure):
@@ -44,7 +47,8 @@ class ShapeOut(C.Structure):
                 ("depth", C.c_int32), ("func", C.c_int32), ("pad0", C.c_int32),
                 ("direct", C.c_double * 16), ("inverse", C.c_double * 16),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
-                ("step", C.c_double)]
+                ("step", C.c_double), ("fa", C.c_double), ("fb", C.c_double), ("fc", C.c_double),
+                ("fd", C.c_double), ("fr", C.c_double)]
 
 
 class Hit(C.Structure):
@@ -203,10 +207,15 @@ def records_from_json(text: str):
         elif t == "Cube":
             r.type = CUBE
         elif t == "BruteForsableShape":
-            if s["shape"]["type"] != "Heart":
-                raise NotImplementedError(s["shape"]["type"])
+            fn = s["shape"]
+            if fn["type"] not in FUNC_IDS:
+                raise NotImplementedError(fn["type"])
             r.type = MARCH
-            r.func = FUNC_HEART
+            r.func = FUNC_IDS[fn["type"]]
+            # BruteForceShapeJson fields (ray_marching.rs:559-670); the Heart has none
+            for k, fld in (("a", "fa"), ("b", "fb"), ("c", "fc"), ("d", "fd"), ("sphere_radius", "fr")):
+                if k in fn and r.func != FUNC_HEART:
+                    setattr(r, fld, float(fn[k]))
             r.step = float(s["step"])
             r.depth = int(s.get("depth", 4))
         else:

@@ -278,6 +278,7 @@ typedef struct {
     int type, material, inverse_normal, depth, func;
     mat4 direct, inverse;
     double x0, y0, x1, y1, step;
+    double fa, fb, fc, fd, fr;
 } shape_t;
 
 typedef struct {
@@ -388,6 +389,11 @@ or_scene *or_scene_new(const or_shape_in *shapes, int n, const or_material_in *m
         sh.x1 = shapes[i].x1;
         sh.y1 = shapes[i].y1;
         sh.step = shapes[i].step;
+        sh.fa = shapes[i].fa;
+        sh.fb = shapes[i].fb;
+        sh.fc = shapes[i].fc;
+        sh.fd = shapes[i].fd;
+        sh.fr = shapes[i].fr;
         transform_new(vload(shapes[i].translate), vload(shapes[i].rotate), vload(shapes[i].scale),
                       &sh.direct, &sh.inverse);
         push_shape(s, sh);
@@ -419,6 +425,11 @@ void or_scene_get_shape(const or_scene *s, int i, or_shape_out *o) {
     o->x1 = sh->x1;
     o->y1 = sh->y1;
     o->step = sh->step;
+    o->fa = sh->fa;
+    o->fb = sh->fb;
+    o->fc = sh->fc;
+    o->fd = sh->fd;
+    o->fr = sh->fr;
 }
 void or_scene_get_material(const or_scene *s, int i, or_material_in *o) {
     const mat_t *m = &s->mats[i];
@@ -557,21 +568,118 @@ static int heart_bound(v3 o, v3 d, double *start, double *end) {
     *end = fmax(x2, 0.0);
     return 1;
 }
+/* Sine::shape_func ray_marching.rs:202-210 */
+static double sine_f(const shape_t *s, v3 p) {
+    return s->fa * s->fa * (p.x - p.y - p.z) * (p.x + p.y - p.z) * (p.x - p.y + p.z) * (p.x + p.y + p.z) +
+           4.0 * p.x * p.x * p.y * p.y * p.z * p.z;
+}
+/* Sine::gradient :227-238 */
+static v3 sine_gradient(const shape_t *s, v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double a2 = s->fa * s->fa;
+    return V(4.0 * p.x * (a2 * (x2 - y2 - z2) + 2.0 * y2 * z2),
+             8.0 * x2 * p.y * z2 - 4.0 * a2 * p.y * (x2 - y2 + z2),
+             8.0 * x2 * y2 * p.z - 4.0 * a2 * p.z * (x2 + y2 - z2));
+}
+/* Star::shape_func :258-264, gradient :279-289 */
+static double star_f(const shape_t *s, v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double c = x2 + y2 + z2 - 1.0;
+    return s->fa * (x2 * y2 + x2 * z2 + y2 * z2) + (c * c * c);
+}
+static v3 star_gradient(const shape_t *s, v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double c = x2 + y2 + z2 - 1.0;
+    return V(2.0 * s->fa * p.x * (y2 + z2) + 6.0 * p.x * c * c, 2.0 * s->fa * p.y * (x2 + z2) + 6.0 * p.y * c * c,
+             2.0 * s->fa * p.z * (x2 + y2) + 6.0 * p.z * c * c);
+}
+/* DupinCyclide::shape_func :339-344, gradient :359-367 */
+static double dupin_f(const shape_t *s, v3 p) {
+    double b2 = s->fb * s->fb;
+    double e = p.x * p.x + p.y * p.y + p.z * p.z + b2 - s->fd * s->fd;
+    double f = s->fa * p.x - s->fc * s->fd;
+    return e * e - 4.0 * (f * f + b2 * p.y * p.y);
+}
+static v3 dupin_gradient(const shape_t *s, v3 p) {
+    double b2 = s->fb * s->fb;
+    double e = 4.0 * (p.x * p.x + p.y * p.y + p.z * p.z + b2 - s->fd * s->fd);
+    return V(e * p.x - 8.0 * s->fa * (s->fa * p.x - s->fc * s->fd), e * p.y - 8.0 * b2 * p.y, e * p.z);
+}
+/* HuntsSurface::shape_func :399-406, gradient :421-433 */
+static double hunts_f(v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double a = x2 + y2 + z2 - 13.0;
+    double b = 3.0 * x2 + y2 - 4.0 * z2 - 12.0;
+    return 4.0 * a * a * a + 27.0 * b * b;
+}
+static v3 hunts_gradient(v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double a = x2 + y2 + z2 - 13.0;
+    double b = 3.0 * x2 + y2 - 4.0 * (z2 + 3.0);
+    return V(24.0 * p.x * a * a + 324.0 * p.x * b, 12.0 * p.y * (2.0 * a * a + 9.0 * b),
+             24.0 * p.z * (a * a - 18.0 * b));
+}
+/* Cushion::shape_func :456-472, gradient :487-496 */
+static double cushion_f(v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    double a = x2 - p.z;
+    return z2 * x2 - z2 * z2 - 2.0 * p.z * x2 + 2.0 * p.z * z2 + x2 - z2 - a * a - y2 * y2 - 2.0 * x2 * y2 - y2 * z2 +
+           2.0 * y2 * p.z + y2;
+}
+static v3 cushion_gradient(v3 p) {
+    double x2 = p.x * p.x, y2 = p.y * p.y, z2 = p.z * p.z;
+    return V(2.0 * p.x * (-2.0 * x2 - 2.0 * y2 + z2 + 1.0),
+             -2.0 * p.y * (2.0 * x2 + 2.0 * y2 + z2 - 2.0 * p.z - 1.0),
+             2.0 * p.z * (x2 - 2.0 * z2 + 3.0 * p.z - 2.0) - 2.0 * p.y * (p.z - 1.0));
+}
+/* ShapeFunction::shape_func dispatch */
+static double func_f(const shape_t *s, v3 p) {
+    switch (s->func) {
+    case OR_FUNC_SINE: return sine_f(s, p);
+    case OR_FUNC_STAR: return star_f(s, p);
+    case OR_FUNC_DUPIN: return dupin_f(s, p);
+    case OR_FUNC_HUNTS: return hunts_f(p);
+    case OR_FUNC_CUSHION: return cushion_f(p);
+    default: return heart_f(p);
+    }
+}
+static v3 func_gradient(const shape_t *s, v3 p) {
+    switch (s->func) {
+    case OR_FUNC_SINE: return sine_gradient(s, p);
+    case OR_FUNC_STAR: return star_gradient(s, p);
+    case OR_FUNC_DUPIN: return dupin_gradient(s, p);
+    case OR_FUNC_HUNTS: return hunts_gradient(p);
+    case OR_FUNC_CUSHION: return cushion_gradient(p);
+    default: return heart_gradient(p);
+    }
+}
+/* intersect_bound of the non-Heart functions (e.g. Sine :212-225): the
+ * sphere_radius ball */
+static int sphere_bound(double radius, v3 o, v3 d, double *start, double *end) {
+    double x1, x2;
+    if (!solve_quadratic(vdot(d, d), vdot(d, o), vdot(o, o) - radius * radius, &x1, &x2)) return 0;
+    if (x1 < 0.0 && x2 < 0.0) return 0;
+    *start = fmax(x1, 0.0);
+    *end = fmax(x2, 0.0);
+    return 1;
+}
+
 /* RayMarchingShape::ray_intersect: ray_marching.rs:20-74 */
 static int march_t(const shape_t *s, v3 o, v3 d, double min_t, double max_t, double *out, or_stats *st) {
     double start, end;
     if (st) st->march_bounds++;
-    if (!heart_bound(o, d, &start, &end)) return 0;
+    if (s->func == OR_FUNC_HEART ? !heart_bound(o, d, &start, &end) : !sphere_bound(s->fr, o, d, &start, &end))
+        return 0;
     double step = s->step;
     double t = start;
     v3 p = vadd(o, vscale(d, t));
-    double r = heart_f(p);
+    double r = func_f(s, p);
     for (int pass = 0; pass < s->depth; pass++) {
         for (;;) {
             if (t > end || t < start) return 0;
             t += step;
             p = vadd(p, vscale(d, step));
-            double next = heart_f(p);
+            double next = func_f(s, p);
             if (st) st->march_steps++;
             if (approx_equal(next, 0.0)) goto done;
             if ((r < 0.0 && next > 0.0) || (r > 0.0 && next < 0.0)) {
@@ -626,7 +734,7 @@ static v3 shape_obj_normal(const shape_t *s, v3 o, v3 d, double t, v3 *p_out) {
     case OR_MARCH: { /* ray_marching.rs:59-60 */
         v3 p = vadd(o, vscale(d, t));
         *p_out = p;
-        return heart_gradient(p);
+        return func_gradient(s, p);
     }
     }
     *p_out = V(NAN, NAN, NAN);
@@ -671,8 +779,13 @@ static void shape_bbox(const shape_t *s, v3 *mn, v3 *mx) {
     switch (s->type) {
     case OR_RECT: lo[0] = s->x0; lo[1] = s->y0; lo[2] = -0.0001; hi[0] = s->x1; hi[1] = s->y1; hi[2] = 0.0001; break;
     case OR_MARCH:
-        lo[0] = -HEART_R; lo[1] = -(HEART_R / 2.05); lo[2] = -HEART_R;
-        hi[0] = HEART_R; hi[1] = HEART_R / 2.05; hi[2] = HEART_R;
+        if (s->func == OR_FUNC_HEART) {
+            lo[0] = -HEART_R; lo[1] = -(HEART_R / 2.05); lo[2] = -HEART_R;
+            hi[0] = HEART_R; hi[1] = HEART_R / 2.05; hi[2] = HEART_R;
+        } else { /* the other functions' get_bounds: the sphere_radius cube (e.g. Sine :244-256) */
+            lo[0] = lo[1] = lo[2] = -s->fr;
+            hi[0] = hi[1] = hi[2] = s->fr;
+        }
         break;
     default: lo[0] = lo[1] = lo[2] = -1.0; hi[0] = hi[1] = hi[2] = 1.0; break;
     }

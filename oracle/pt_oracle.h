@@ -38,6 +38,11 @@ extern "C" {
 
 /* ray-marched implicit functions (src/world/shapes/ray_marching.rs) */
 #define OR_FUNC_HEART 0
+#define OR_FUNC_SINE 1
+#define OR_FUNC_STAR 2
+#define OR_FUNC_DUPIN 3
+#define OR_FUNC_HUNTS 4
+#define OR_FUNC_CUSHION 5
 
 /* materials (src/world/material.rs) */
 #define OR_LAMBERTIAN 0
@@ -51,6 +56,7 @@ typedef struct {
     int32_t func, pad0;
     double translate[3], rotate[3], scale[3];
     double x0, y0, x1, y1, step;
+    double fa, fb, fc, fd, fr; /* ray-marched function: a, b, c, d, sphere_radius */
 } or_shape_in;
 
 typedef struct {
@@ -65,6 +71,7 @@ typedef struct {
     int32_t type, material, inverse_normal, depth, func, pad0;
     double direct[16], inverse[16];
     double x0, y0, x1, y1, step;
+    double fa, fb, fc, fd, fr;
 } or_shape_out;
 
 typedef struct {

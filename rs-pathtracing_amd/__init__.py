@@ -67,7 +67,8 @@ class ShapeInfo(C.Structure):
                 ("depth", C.c_int32), ("func", C.c_int32), ("pad0", C.c_int32),
                 ("direct", C.c_double * 16), ("inverse", C.c_double * 16),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
-                ("step", C.c_double)]
+                ("step", C.c_double), ("a", C.c_double), ("b", C.c_double), ("c", C.c_double), ("d", C.c_double),
+                ("sphere_radius", C.c_double)]
 
 
 class MaterialInfo(C.Structure):
@@ -373,8 +374,8 @@ def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
 
 def wave_diag(renderer: "HipRenderer", enable: bool = True):
     """Read-and-clear the wavefront march kernel's phase diagnostics (pt_wave_diag)."""
-    out = (C.c_uint64 * 36)()
-    _check(lib().pt_wave_diag(renderer._h, 1 if enable else 0, out, 36))
+    out = (C.c_uint64 * 40)()
+    _check(lib().pt_wave_diag(renderer._h, 1 if enable else 0, out, 40))
     return list(out)
 
 

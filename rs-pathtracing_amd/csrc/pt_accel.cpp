@@ -20,8 +20,14 @@ DBox shape_box(const HostShape &s) {
         hi[0] = s.x1; hi[1] = s.y1; hi[2] = 0.0001;
         break;
     case MARCH:
-        lo[0] = -1.45; lo[1] = -(1.45 / 2.05); lo[2] = -1.45;
-        hi[0] = 1.45; hi[1] = 1.45 / 2.05; hi[2] = 1.45;
+        if (s.func == 0) {  // Heart: the fixed ellipsoid bound (ray_marching.rs:126-145)
+            lo[0] = -1.45; lo[1] = -(1.45 / 2.05); lo[2] = -1.45;
+            hi[0] = 1.45; hi[1] = 1.45 / 2.05; hi[2] = 1.45;
+        } else {  // the other functions: the sphere_radius ball
+            const double r = std::fabs(s.fr);
+            lo[0] = lo[1] = lo[2] = -r;
+            hi[0] = hi[1] = hi[2] = r;
+        }
         break;
     default:
         lo[0] = lo[1] = lo[2] = -1.0;

@@ -136,6 +136,11 @@ int pt_scene_get_shape(const pt_scene *s, int i, pt_shape_info *o) {
     o->x1 = h.x1;
     o->y1 = h.y1;
     o->step = h.step;
+    o->a = h.fa;
+    o->b = h.fb;
+    o->c = h.fc;
+    o->d = h.fd;
+    o->sphere_radius = h.fr;
     return PT_OK;
 }
 int pt_scene_get_material(const pt_scene *s, int i, pt_material_info *o) {
@@ -207,6 +212,9 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     r->ds.nnodes = (int)acc.nodes.size();
     r->ds.nlin = (int)acc.lin.size();
     r->ds.nmarch = (int)acc.march.size();
+    r->ds.fkind = 0;  // Heart-only kernel builds unless another function is marched
+    for (const auto &h : r->scene->s.shapes)
+        if (h.type == MARCH && h.func != 0) r->ds.fkind = -1;
     *out = r;
     return PT_OK;
 }
@@ -475,9 +483,9 @@ int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(r->device));
     HIP_TRY(hipStreamSynchronize(r->stream));
-    if (out && n && r->ws.diag) HIP_TRY(hipMemcpy(out, r->ws.diag, (n < 36 ? n : 36) * 8, hipMemcpyDeviceToHost));
-    if (enable && !r->ws.diag) HIP_TRY(hipMalloc(&r->ws.diag, 36 * 8));
-    if (r->ws.diag) HIP_TRY(hipMemset(r->ws.diag, 0, 36 * 8));
+    if (out && n && r->ws.diag) HIP_TRY(hipMemcpy(out, r->ws.diag, (n < 40 ? n : 40) * 8, hipMemcpyDeviceToHost));
+    if (enable && !r->ws.diag) HIP_TRY(hipMalloc(&r->ws.diag, 40 * 8));
+    if (r->ws.diag) HIP_TRY(hipMemset(r->ws.diag, 0, 40 * 8));
     if (!enable && r->ws.diag) {
         HIP_TRY(hipFree(r->ws.diag));
         r->ws.diag = nullptr;

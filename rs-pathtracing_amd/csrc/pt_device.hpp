@@ -136,23 +136,61 @@ PT_HD V3 heart_gradient(V3 p) {
               2.0 * p.z * (a - p.z * (1.5 * p.x * p.x + (27.0 / 40.0) * p.y * p.y)));
 }
 
+// The implicit function of a ray-marched shape.
+PT_HD march::FParams shape_params(const DShape &S) {
+    march::FParams F;
+    F.func = S.func;
+    F.pad = 0;
+    F.k[0] = S.fk[0];
+    F.k[1] = S.fk[1];
+    F.k[2] = S.fk[2];
+    F.k[3] = S.fk[3];
+    F.radius = S.fradius;
+    return F;
+}
+
 // ------------------------------------------------------------ closest hit
 struct Ray {
     V3 o, d;
 };
 
-template <bool STATS>
+#ifndef PT_LAZY_RECT
+#define PT_LAZY_RECT 1
+#endif
+// MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
+// every one on the march list), so the march branch is not compiled in.
+template <bool STATS, int FK = march::F_ANY, bool MARCHED = true>
 PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct) {
+    if (STATS) ct->c[C_TEST_SPHERE + s.type]++;
+    if (PT_LAZY_RECT && s.type == RECTANGLE) {
+        // Rectangle: t needs only the object-space z row; x and y are
+        // transformed only for a t in range.  Each component is the same
+        // expression as in xf_point / xf_vector, so every value is unchanged.
+        const double *m = s.inv;
+        const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
+        const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
+        const double tt = -oz / dz;
+        if (tt < min_t || tt > max_t) return false;
+        const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
+        const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
+        const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
+        const double dy = r.d.x * m[4] + r.d.y * m[5] + r.d.z * m[6];
+        const double px = ox + dx * tt, py = oy + dy * tt;
+        if (px < s.p[0] || px > s.p[2] || py < s.p[1] || py > s.p[3]) return false;
+        *t = tt;
+        return true;
+    }
     V3 o = xf_point(s.inv, r.o);  // inverse_transform_ray (transform.rs:32-37), no renormalisation
     V3 d = xf_vector(s.inv, r.d);
-    if (STATS) ct->c[C_TEST_SPHERE + s.type]++;
     switch (s.type) {
     case SPHERE: return sphere_t(o, d, min_t, max_t, t);
     case RECTANGLE: return rect_t(s.p, o, d, min_t, max_t, t);
     case CUBE: return cube_t(o, d, min_t, max_t, t);
     default: {
+        if (!MARCHED) return false;
         march::MarchStats ms{0, 0, 0};
-        bool h = march::heart_march<STATS>(s.p[0], s.depth, o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t, t, &ms);
+        bool h = march::func_march<STATS, FK>(shape_params(s), s.p[0], s.depth, o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t,
+                                          t, &ms);
         if (STATS) {
             ct->c[C_MARCH_STEPS] += ms.steps;
             ct->c[C_MARCH_BLOCKS] += ms.blocks;
@@ -199,7 +237,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     for (int k = 0; k < sc.nlin; k++) {
         int i = sc.lin[k];
         double t;
-        if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+        if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
             best = t;
             who = i;
         }
@@ -213,7 +251,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
             for (int k = 0; k < nd.count; k++) {
                 int i = sc.leaf[nd.first + k];
                 double t;
-                if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+                if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
                     best = t;
                     who = i;
                 }
@@ -255,6 +293,7 @@ struct Hit {
 };
 // ray_hit_transformed (shapes/mod.rs:112-124): world point = direct * p_obj,
 // world normal = inverse^T * normalize(n_obj), then RayHit::set_normal (ray.rs:60-64).
+template <int FK = march::F_ANY>
 PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
     V3 o = xf_point(s.inv, r.o);
     V3 d = xf_vector(s.inv, r.d);
@@ -272,7 +311,12 @@ PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
         else n = v3(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
         break;
     }
-    default: n = heart_gradient(p); break;  // ray_marching.rs:59-60
+    default: {  // ray_marching.rs:59-60: the function's gradient at p
+        double g[3];
+        march::shape_gradient_k<FK>(shape_params(s), p.x, p.y, p.z, g);
+        n = v3(g[0], g[1], g[2]);
+        break;
+    }
     }
     n = normalize(n);  // RayHit::new (ray.rs:32-52)
     V3 wn = xf_normal(s.inv, n);
@@ -356,7 +400,7 @@ struct IdStack {
 // Everything in a bounce after the closest hit (who, t) is known.
 // Stack: any type with push(id), pop() and a count n (IdStack in registers,
 // or the wavefront engine's per-slot id array in HBM).
-template <bool STATS = false, class Stack>
+template <bool STATS = false, int FK = march::F_ANY, class Stack>
 PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, Stack &stk, Rng &rng,
                  double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
@@ -369,7 +413,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     }
     const DShape &s = sc.shapes[who];
     if (STATS) ct->c[C_HITS]++;
-    Hit h = finish(s, ray, t);
+    Hit h = finish<FK>(s, ray, t);
     const DMaterial &m = sc.mats[s.material];
     if (tfin) *tfin = PT_STAMP();
     V3 dir;
@@ -468,7 +512,7 @@ constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
 enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
 
 
-template <int NW, bool STATS = false, bool TIMING = false>
+template <int NW, bool STATS = false, bool TIMING = false, int FK = march::F_ANY>
 PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr,
                      PhaseTimes *pt = nullptr) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
@@ -508,7 +552,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_MARCH) {
             if (TIMING) pt->march_passes++;
             for (int it = 0; it < MARCH_ITERS; it++) {
-                int st = march::march_iter<STATS>(ms, &mst);
+                int st = march::march_iter<STATS, true, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                     if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
@@ -535,7 +579,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                 const DShape &S = sc.shapes[i];
                 if (STATS) ct->c[C_TEST_MARCH]++;
                 V3 o = xf_point(S.inv, ray.o), d = xf_vector(S.inv, ray.d);
-                if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
+                if (march::march_begin<FK>(shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
                     mshape = i;
                     phase = PH_MARCH;
                     break;
@@ -550,7 +594,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_SHADE) {
             V3 leaf;
             uint64_t tf = 0;
-            const bool ended = shade<STATS>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
+            const bool ended = shade<STATS, FK>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
                                                 TIMING ? &tf : nullptr);
             if (TIMING) {
                 uint64_t n = PT_STAMP();

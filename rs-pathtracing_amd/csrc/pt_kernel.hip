@@ -24,7 +24,7 @@ using dev::V3;
 
 // WAVES = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__' second argument): 2 -> <= 256 VGPRs, 3 -> <= 168, 4 -> <= 128.
-template <int NW, int WAVES>
+template <int NW, int WAVES, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
     const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
     const uint32_t k = P.rank + ti * P.world;       // global tile id
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameP
         if (P.compact) dst[0] = dst[1] = dst[2] = 0.0;
         return;
     }
-    V3 c = dev::trace_pixel<NW>(sc, P, x, y);
+    V3 c = dev::trace_pixel<NW, false, false, FK>(sc, P, x, y);
     dst[0] = c.x;
     dst[1] = c.y;
     dst[2] = c.z;
@@ -138,7 +138,9 @@ __global__ __launch_bounds__(256) void march_probe(const double *__restrict__ jo
     march::MarchState m;
     int st = march::M_MISS;
     uint32_t k = 0;
-    if (march::march_begin(j[0], (int)j[1], j[2], j[3], j[4], j[5], j[6], j[7], &m)) {
+    march::FParams F{};
+    F.func = march::F_HEART;
+    if (march::march_begin(F, j[0], (int)j[1], j[2], j[3], j[4], j[5], j[6], j[7], &m)) {
         march::MarchStats ms{0, 0, 0};
         while ((st = march::march_iter<false>(m, &ms)) == march::M_RUNNING) k++;
     }
@@ -240,7 +242,7 @@ static int render_waves() {
 }
 
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
-                              WaveWorkspace *ws);
+                              WaveWorkspace *ws, int fkind);
 
 static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
     const char *e = getenv("PT_ENGINE");
@@ -252,16 +254,19 @@ static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
                          WaveWorkspace *ws) {
     if (P.tile_count == 0) return hipSuccess;
-    if (use_wavefront(s, ws)) return launch_render_wave(dscene(s), P, out, st, ws);
+    if (use_wavefront(s, ws)) return launch_render_wave(dscene(s), P, out, st, ws, s.fkind);
     KernelTimer *tm = ws ? ws->timer : nullptr;
     hipError_t e0 = timer_begin(tm, st, K_MEGA);
     if (e0 != hipSuccess) return e0;
-    if (P.depth <= 8) {
+    if (P.depth <= 8 && s.fkind == march::F_HEART) {
+        // Heart-only (or no marched shape): the single-function build
         switch (render_waves()) {
-        case 2: render_tiles<4, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
-        case 3: render_tiles<4, 3><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
-        default: render_tiles<4, 4><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        case 2: render_tiles<4, 2, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        case 3: render_tiles<4, 3, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        default: render_tiles<4, 4, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         }
+    } else if (P.depth <= 8) {
+        render_tiles<4, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out);
     } else {
         PT_DISPATCH_NW(P.depth, (render_tiles<NW, 2><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out)));
     }

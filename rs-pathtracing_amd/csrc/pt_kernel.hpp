@@ -14,6 +14,7 @@ struct DeviceScene {
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
+    int fkind = 0;  // 0: every marched shape is a Heart (or none) -> Heart-only kernel builds; -1: any
 };
 
 // Device workspace of the wavefront engine (pt_wave.hip), grown on demand and

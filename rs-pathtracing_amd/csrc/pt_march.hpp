@@ -27,6 +27,8 @@
 #include <cmath>
 #include <cstdint>
 
+#include "pt_funcs.hpp"
+
 #ifndef PT_HD
 #define PT_HD __host__ __device__ __forceinline__
 #endif
@@ -45,40 +47,14 @@
 namespace pt {
 namespace march {
 
-// Heart::shape_func (ray_marching.rs:147-155)
-PT_HD double heart_f(double px, double py, double pz) {
-    double x2 = px * px;
-    double y2 = py * py;
-    double z2 = pz * pz;
-    double z3 = z2 * pz;
-    double a = x2 + (9.0 / 4.0) * y2 + z2 - 1.0;
-    return a * a * a - x2 * z3 - (9.0 / 80.0) * y2 * z3;
-}
-
-// Heart::intersect_bound (:135-145) + solve_quadratic_equation (algebra/equation.rs:5-15)
+// Heart::shape_func and Heart::intersect_bound (ray_marching.rs:135-155), as
+// FParams-free helpers (tests, tools); the march itself is generic.
+PT_HD double heart_f(double px, double py, double pz) { return f_heart(px, py, pz); }
 PT_HD bool heart_bound(double ox, double oy, double oz, double dx, double dy, double dz, double *start,
                        double *end) {
-    const double rx = 1.45, ry = 1.45 / 2.05, rz = 1.45;
-    double oox = ox / rx, ooy = oy / ry, ooz = oz / rz;
-    double ddx = dx / rx, ddy = dy / ry, ddz = dz / rz;
-    double a = ddx * ddx + ddy * ddy + ddz * ddz;
-    double hb = ddx * oox + ddy * ooy + ddz * ooz;
-    double c = oox * oox + ooy * ooy + ooz * ooz - 1.0;
-    double disc = hb * hb - a * c;
-    if (disc < 0.0) return false;
-    double x1, x2;
-    if (disc == 0.0) {
-        x1 = -hb;
-        x2 = -hb;
-    } else {
-        double sq = sqrt(disc);
-        x1 = (-hb - sq) / a;
-        x2 = (-hb + sq) / a;
-    }
-    if (x1 < 0.0 && x2 < 0.0) return false;
-    *start = fmax(x1, 0.0);
-    *end = fmax(x2, 0.0);
-    return true;
+    FParams F{};
+    F.func = F_HEART;
+    return shape_bound(F, ox, oy, oz, dx, dy, dz, start, end);
 }
 
 // ------------------------------------------------------- closed-form adds
@@ -290,6 +266,9 @@ struct Poly {
     double ax, ay, az, cx, cy, cz;     // |p0|, |ch| for the magnitude bound
 };
 
+// The Heart's expansion, by coefficient (fewer live temporaries than the
+// generic degree-tracked expansion; both are exact-arithmetic expansions of
+// the same polynomial, with rounding inside the proof's margin).
 PT_HD void heart_poly(double x, double y, double z, double cx, double cy, double cz, Poly *P) {
     double x2[3] = {x * x, 2.0 * x * cx, cx * cx};
     double y2[3] = {y * y, 2.0 * y * cy, cy * cy};
@@ -325,6 +304,22 @@ PT_HD void heart_poly(double x, double y, double z, double cx, double cy, double
     P->cz = fabs(cz);
 }
 
+// The expansion for any of the ray-marched functions (pt_funcs.hpp).
+template <int FK>
+PT_HD void func_poly(const FParams &F, double x, double y, double z, double cx, double cy, double cz, Poly *P) {
+    if constexpr (FK == F_HEART) {
+        heart_poly(x, y, z, cx, cy, cz, P);
+        return;
+    }
+    shape_poly_k<FK>(F, x, y, z, cx, cy, cz, P->g);
+    P->ax = fabs(x);
+    P->ay = fabs(y);
+    P->az = fabs(z);
+    P->cx = fabs(cx);
+    P->cy = fabs(cy);
+    P->cz = fabs(cz);
+}
+
 // True if sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither
 // the approx_equal stop nor a sign change can fire inside the block).
 //  * margin: 1e-15 + 256 eps M(b), where M(b) bounds the magnitudes of all
@@ -334,16 +329,15 @@ PT_HD void heart_poly(double x, double y, double z, double cx, double cy, double
 //    (with the same kind of margin), g is monotone there and its extreme on
 //    [1, b] is g(b) (decreasing) or at least g(0) (increasing);
 //  * otherwise the absolute Taylor bound g0 - sum_k |g_k| b^k.
-PT_HD double poly_mag(const Poly &P, double b) {
+PT_HD double heart_mag(const Poly &P, double b) {
     double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
     double x2 = xm * xm, y2 = ym * ym, z2 = zm * zm, z3 = z2 * zm;
     double am = x2 + 2.25 * y2 + z2 + 1.0;
     return am * am * am + x2 * z3 + 0.1125 * y2 * z3;
 }
-
-PT_HD double poly_margin(const Poly &P, double b) {
+PT_HD double heart_margin(const Poly &P, double b) {
     const double e256 = 2.8421709430404007e-14;  // 256 * 2^-53
-    double mag = poly_mag(P, b);
+    double mag = heart_mag(P, b);
     // The step points are p_j = p0 + j*c + delta_j with |delta_j,k| <= j*ulp_k/2
     // (each literal add rounds once): add max|grad f| . |delta| over the block.
     double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
@@ -356,13 +350,28 @@ PT_HD double poly_margin(const Poly &P, double b) {
     return 1e-15 + e256 * mag + drift;
 }
 
+template <int FK>
+PT_HD double poly_margin(const FParams &F, const Poly &P, double b) {
+    if constexpr (FK == F_HEART) return heart_margin(P, b);
+    const double e256 = 2.8421709430404007e-14;  // 256 * 2^-53
+    const double xm = P.ax + P.cx * b, ym = P.ay + P.cy * b, zm = P.az + P.cz * b;
+    // M(b) bounds every monomial of f over the block (|f| and its f64
+    // evaluation error scale); G bounds |df/dx_k| there.  The step points are
+    // p_j = p0 + j*c + delta_j with |delta_j,k| <= j*ulp_k/2 (each literal
+    // add rounds once): add max|grad f| . |delta| over the block.
+    const DM m = shape_mag_k<FK>(F, xm, ym, zm);
+    const double drift = b * 2.3e-16 * (m.gx * xm + m.gy * ym + m.gz * zm);  // ulp(v)/2 <= 2^-53 |v|
+    return 1e-15 + e256 * m.v + drift;
+}
+
 // Bernstein form of sgn*g on j in [0, b] (lambda = j / b): g >= min_i beta_i
 // over the whole block (convex hull property), and min beta = g(b) exactly
 // when the control polygon is monotone, so the test is tight for the usual
 // monotone approach to the surface.  The betas' own rounding (weights <= 1,
 // at most 7 terms) is far inside the 256 eps M(b) part of the margin.
-PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
-    const double margin = poly_margin(P, b);
+template <int FK = F_ANY>
+PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double sgn) {
+    const double margin = poly_margin<FK>(F, P, b);
     double a[7];
     double bk = 1.0;
 #pragma unroll
@@ -395,9 +404,10 @@ PT_HD bool poly_sign_definite(const Poly &P, double b, double sgn) {
 // descends into it.  The margin is the one for the whole block (M and the
 // drift only grow with b), and the halving's own rounding (<= 24 levels of
 // exact-weight averages) stays far inside its 256 eps M part.
-PT_HD int64_t poly_prefix(const Poly &P, int64_t B, double sgn) {
+template <int FK>
+PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn) {
     const double Bd = (double)B;
-    const double margin = poly_margin(P, Bd);
+    const double margin = poly_margin<FK>(F, P, Bd);
     double a[7];
     double bk = 1.0;
 #pragma unroll
@@ -531,6 +541,7 @@ struct MarchStats {
 // a lane can march a few iterations per pass of the kernel's main loop while
 // the other lanes of its wave keep tracing.
 struct MarchState {
+    FParams F;  // which implicit function, and its constants
     double t, px, py, pz, r, s, start, end, dx, dy, dz;
     int64_t lim;  // steps_in_range from the current point for this pass (-1: not known yet)
     int pass, passes;
@@ -543,10 +554,12 @@ enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2 };
 constexpr uint32_t MARCH_GUARD = 1u << 24;
 
 // Bound test and start of the march; false if the ray misses the bound.
-PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
-                       MarchState *m) {
+template <int FK = F_ANY>
+PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, double oy, double oz, double dx,
+                       double dy, double dz, MarchState *m) {
     double start, end;
-    if (!heart_bound(ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+    if (!shape_bound_k<FK>(F, ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+    m->F = F;
     PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz);
     m->start = start;
     m->end = end;
@@ -555,7 +568,7 @@ PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz
     m->px = ox + dx * start;
     m->py = oy + dy * start;
     m->pz = oz + dz * start;
-    m->r = heart_f(m->px, m->py, m->pz);
+    m->r = shape_f_k<FK>(F, m->px, m->py, m->pz);
     m->dx = dx;
     m->dy = dy;
     m->dz = dz;
@@ -571,6 +584,7 @@ PT_HD bool march_begin(double step0, int passes, double ox, double oy, double oz
 // One round of a proven block's exact advance: one binade segment for each
 // of t, px, py, pz that still has steps to go; when all are done the block's
 // end point is exact and f is evaluated there.
+template <int FK = F_ANY>
 PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
     PT_MHOOK(block_begin);
     for (int round = 0; round < PT_ADV_ROUNDS; round++) {
@@ -582,13 +596,13 @@ PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
     }
     if (m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0) return;
     m.adv = 0;
-    m.r = heart_f(m.px, m.py, m.pz);
+    m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
 }
 
 // One iteration of the march loop: a proven jump, or one literal step (after a
 // failed proof).  M_DONE: the passes ended (the caller applies the final
 // t-in-[min_t, max_t] test); M_MISS: t left [start, end].
-template <bool STATS, bool INLINE_ADV = true>
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
     PT_MPROF(iters);
     if (m.pass >= m.passes) return M_DONE;
@@ -599,7 +613,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
     double s = m.s;
     double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
     if (m.adv) {
-        march_advance(m, cx, cy, cz);
+        march_advance<FK>(m, cx, cy, cz);
         return M_RUNNING;
     }
     if (m.t > m.end || m.t < m.start) return M_MISS;
@@ -614,7 +628,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
         const int64_t bmax = m.lim;
         if (bmax >= 2) {
             Poly P;
-            heart_poly(m.px, m.py, m.pz, cx, cy, cz, &P);
+            func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
             if (STATS) st->tries++;
             // longest provable prefix of a block sized from the predicted
             // crossing (the margin scales with the block, so a block far
@@ -628,7 +642,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
             int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
             if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
-            int64_t good = poly_prefix(P, B, sgn);
+            int64_t good = poly_prefix<FK>(m.F, P, B, sgn);
             if (ub < BIG && good >= ub) return M_MISS;
             good = good > bmax ? bmax : good;
             if (good >= 2) {
@@ -649,7 +663,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     m.pz = advance(m.pz, cz, good);
                     m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
                     m.adv = 0;
-                    m.r = heart_f(m.px, m.py, m.pz);
+                    m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
                     // a prefix that stopped short of B ends just before the
                     // crossing: take that literal step in this iteration
                     if (PT_FOLD_LIT && good < B && m.lim >= 1) goto literal;
@@ -665,7 +679,7 @@ literal:
     m.px += cx;
     m.py += cy;
     m.pz += cz;
-    double next = heart_f(m.px, m.py, m.pz);
+    double next = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
     if (STATS) st->steps++;
     if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
         m.pass = m.passes;
@@ -699,18 +713,26 @@ PT_HD int march_phase(MarchState &m) {
 
 // RayMarchingShape::ray_intersect for the Heart in object space (o, d):
 // returns true with *t_out on a hit in [min_t, max_t].
-template <bool STATS>
-PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
-                       double min_t, double max_t, double *t_out, MarchStats *st) {
+template <bool STATS, int FK = F_ANY>
+PT_HD bool func_march(const FParams &F, double step0, int passes, double ox, double oy, double oz, double dx,
+                      double dy, double dz, double min_t, double max_t, double *t_out, MarchStats *st) {
     MarchState m;
-    if (!march_begin(step0, passes, ox, oy, oz, dx, dy, dz, &m)) return false;
+    if (!march_begin<FK>(F, step0, passes, ox, oy, oz, dx, dy, dz, &m)) return false;
     int status;
-    while ((status = march_iter<STATS>(m, st)) == M_RUNNING) {
+    while ((status = march_iter<STATS, true, FK>(m, st)) == M_RUNNING) {
     }
     if (status == M_MISS) return false;
     if (m.t < min_t || m.t > max_t) return false;  // ray_marching.rs:55-57
     *t_out = m.t;
     return true;
+}
+
+template <bool STATS>
+PT_HD bool heart_march(double step0, int passes, double ox, double oy, double oz, double dx, double dy, double dz,
+                       double min_t, double max_t, double *t_out, MarchStats *st) {
+    FParams F{};
+    F.func = F_HEART;
+    return func_march<STATS, F_HEART>(F, step0, passes, ox, oy, oz, dx, dy, dz, min_t, max_t, t_out, st);
 }
 
 }  // namespace march

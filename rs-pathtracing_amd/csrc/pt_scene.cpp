@@ -202,6 +202,17 @@ DShape to_device(const HostShape &s) {
         d.p[3] = s.y1;
     } else if (s.type == MARCH) {
         d.p[0] = s.step;
+        // constants shape_func computes from the parameters (pure, so the
+        // same values): Sine/Star a; DupinCyclide a, b*b, c*d, d*d
+        if (s.func == 3) {
+            d.fk[0] = s.fa;
+            d.fk[1] = s.fb * s.fb;
+            d.fk[2] = s.fc * s.fd;
+            d.fk[3] = s.fd * s.fd;
+        } else {
+            d.fk[0] = s.fa;
+        }
+        d.fradius = s.fr;
     }
     d.type = s.type;
     d.material = s.material;
@@ -431,11 +442,24 @@ Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_
             transform(field(s, "transform"), h);
             const Value &fn = field(s, "shape");
             std::string ft = str(field(fn, "type"), "type");
+            // BruteForceShapeJson variants (ray_marching.rs:559-670); the
+            // Heart has no fields (its bound radii are fixed, :126-131)
             if (ft == "Heart") {
                 h.func = 0;
-            } else if (ft == "Sine" || ft == "Star" || ft == "DupinCyclide" || ft == "HuntsSurface" ||
-                       ft == "Cushion") {
-                unsupported("ray-marched shape `" + ft + "` is not implemented on the GPU path");
+            } else if (ft == "Sine" || ft == "Star") {
+                h.func = ft == "Sine" ? 1 : 2;
+                h.fa = num(field(fn, "a"), "a");
+                h.fr = num(field(fn, "sphere_radius"), "sphere_radius");
+            } else if (ft == "DupinCyclide") {
+                h.func = 3;
+                h.fa = num(field(fn, "a"), "a");
+                h.fb = num(field(fn, "b"), "b");
+                h.fc = num(field(fn, "c"), "c");
+                h.fd = num(field(fn, "d"), "d");
+                h.fr = num(field(fn, "sphere_radius"), "sphere_radius");
+            } else if (ft == "HuntsSurface" || ft == "Cushion") {
+                h.func = ft == "HuntsSurface" ? 4 : 5;
+                h.fr = num(field(fn, "sphere_radius"), "sphere_radius");
             } else {
                 schema("unknown variant `" + ft + "` of BruteForceShapeJson");
             }

@@ -1,7 +1,7 @@
 // pt_types.hpp — device-visible layouts shared by the host library and the
 // HIP kernels.  One DShape per leaf of the realized shape list (JSON shapes in
-// file order, then the add_random_spheres spheres), 256 B each so a shape is
-// four 64-B lines; matrices keep only the three rows the kernels apply.
+// file order, then the add_random_spheres spheres), 320 B each (five 64-B
+// lines); matrices keep only the three rows the kernels apply.
 #pragma once
 #include <cstdint>
 
@@ -16,8 +16,11 @@ struct alignas(64) DShape {
     double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step
     int32_t type, material, inverse_normal, depth;
     int32_t func, pad[3];
+    double fk[4];    // RayMarchingShape function constants (pt_funcs.hpp FParams::k)
+    double fradius;  // its bound's sphere_radius
+    double pad2[3];
 };
-static_assert(sizeof(DShape) == 256, "DShape is four cache lines");
+static_assert(sizeof(DShape) == 320, "DShape is five cache lines");
 
 struct alignas(8) DMaterial {
     int32_t type, pad;

@@ -103,12 +103,23 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 #endif
 
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
-template <int NW, bool FIRST, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it) {
+// DIAG: wave-level s_memtime cycles per section (load + shade, trace,
+// march pre-check, stores) summed into diag[36..39] (tuning only).
+template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY>
+__global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
+                                                        unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
     const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
+    unsigned long long dsec[4] = {0, 0, 0, 0}, tst = 0;
+#define PT_BSTAMP(k)                                         \
+    if (DIAG) {                                              \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+        dsec[k] += n_ - tst;                                 \
+        tst = n_;                                            \
+    }
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
+        if (DIAG) tst = __builtin_amdgcn_s_memtime();
         const uint32_t i = base + threadIdx.x;
         bool live = i < count;
         uint32_t id = 0;
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 V3 leaf;
-                if (dev::shade(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                if (dev::shade<false, FK>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
                     const V3 c = dev::unwind(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
@@ -147,12 +158,14 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 }
             }
         }
+        PT_BSTAMP(0)
         bool need_march = false;
         if (live) {
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
             dev::closest_nomarch(sc, ray, inv, T_MIN, &best, &who);
+            PT_BSTAMP(1)
             // does any marched shape's bound start before the best hit? (the
             // march kernel repeats this select and marches)
             for (int k = 0; k < sc.nmarch && !need_march; k++) {
@@ -162,8 +175,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const DShape &S = sc.shapes[s];
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
-                need_march = march::heart_bound(o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
+                need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
             }
+            PT_BSTAMP(2)
             v.ox[id] = ray.o.x;
             v.oy[id] = ray.o.y;
             v.oz[id] = ray.o.z;
@@ -176,7 +190,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             v.meta[id] = depth | ((uint32_t)stk.n << 8);
         }
         if (i < count) v.status[id] = live ? (need_march ? 3u : 1u) : 0u;
+        PT_BSTAMP(3)
     }
+#undef PT_BSTAMP
+    if (DIAG && (threadIdx.x & 63) == 0)
+        for (int k = 0; k < 4; k++) atomicAdd(&diag[36 + k], dsec[k]);
 }
 
 // Order-preserving compaction of the status bytes into the two id lists
@@ -299,21 +317,11 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 5  // waves per SIMD the march kernel's registers must allow
 #endif
-#ifndef PT_WF_LDS_SHAPES
-#define PT_WF_LDS_SHAPES 0  // marched shapes staged in LDS (measured slower than the L2-cached scene: off)
-#endif
-constexpr int WF_MAXM = PT_WF_LDS_SHAPES > 0 ? PT_WF_LDS_SHAPES : 1;  // marched shapes staged in LDS
-
 struct MarchJob {
     uint32_t id;
     Ray ray;
     double best;
     int who;
-};
-
-struct LdsShape {
-    double lo[3], hi[3], inv[12], step;
-    int depth, index;
 };
 
 __device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob *j) {
@@ -327,26 +335,10 @@ __device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob 
 // DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
 // 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
-template <bool DIAG>
+template <bool DIAG, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag) {
     __shared__ uint32_t head;
-    __shared__ LdsShape msh[WF_MAXM];
     const int nm = sc.nmarch;
-    const int nms = PT_WF_LDS_SHAPES == 0 ? 0 : (nm < WF_MAXM ? nm : WF_MAXM);
-    for (int k = threadIdx.x; k < nms * 24; k += blockDim.x) {
-        const int i = k / 24, f = k % 24, s = sc.march[i];
-        double val;
-        if (f < 3) val = sc.boxes[s].lo[f];
-        else if (f < 6) val = sc.boxes[s].hi[f - 3];
-        else if (f < 18) val = sc.shapes[s].inv[f - 6];
-        else val = sc.shapes[s].p[0];
-        double *dst = f < 3 ? &msh[i].lo[f] : f < 6 ? &msh[i].hi[f - 3] : f < 18 ? &msh[i].inv[f - 6] : &msh[i].step;
-        if (f < 19) *dst = val;
-        if (f == 19) {
-            msh[i].depth = sc.shapes[s].depth;
-            msh[i].index = s;
-        }
-    }
     const uint32_t count = v.cnt[it * 4 + 1];
     const uint32_t *mq = v.mq;
     const uint32_t per = (count + gridDim.x - 1) / gridDim.x;
@@ -421,7 +413,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
             bool done = false;
             if (marching) {
-                const int st = march::march_iter<false, PT_WF_VOTE == 0>(ms, &mst);
+                const int st = march::march_iter<false, PT_WF_VOTE == 0, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                     if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
@@ -434,27 +426,16 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             } else {
                 // select: next marched shape whose bound is entered before `best`
                 while (km < nm) {
-                    const int k = km++;
-                    if (k < nms) {
-                        const LdsShape &S = msh[k];
-                        if (!dev::slab(S.lo, S.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                        const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                        if (march::march_begin(S.step, S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                            mshape = S.index;
-                            marching = true;
-                            break;
-                        }
-                    } else {
-                        const int s = sc.march[k];
-                        const DBox &b = sc.boxes[s];
-                        if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                        const DShape &S = sc.shapes[s];
-                        const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                        if (march::march_begin(S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z, &ms)) {
-                            mshape = s;
-                            marching = true;
-                            break;
-                        }
+                    const int s = sc.march[km++];
+                    const DBox &b = sc.boxes[s];
+                    if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
+                    const DShape &S = sc.shapes[s];
+                    const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
+                    if (march::march_begin<FK>(dev::shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y,
+                                               d.z, &ms)) {
+                        mshape = s;
+                        marching = true;
+                        break;
                     }
                 }
                 done = !marching;
@@ -621,21 +602,29 @@ static int bounce_waves() {
 
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
-                          const WfView &v, int it) {
+                          const WfView &v, int it, unsigned long long *diag, int fkind) {
+    if (fkind != march::F_HEART) {  // another ray-marched function: the generic build
+        wf_bounce<NW, FIRST, 2, false, march::F_ANY><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        return;
+    }
+    if (diag) {
+        wf_bounce<NW, FIRST, 2, true, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it, diag);
+        return;
+    }
     if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
-        wf_bounce<NW, FIRST, 2><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
     }
     switch (bounce_waves()) {
-    case 2: wf_bounce<NW, FIRST, 2><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    case 4: wf_bounce<NW, FIRST, 4><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    default: wf_bounce<NW, FIRST, 3><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    default: wf_bounce<NW, FIRST, 3, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     }
 }
 
 template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
-                                 WaveWorkspace *ws) {
+                                 WaveWorkspace *ws, int fkind) {
     const uint32_t cap_want = wf_cap_paths();
     // tile groups (only for frames beyond cap_want pixels), then sample chunks
     const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
@@ -691,7 +680,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
         }
         int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march<false>, 256, 0) == hipSuccess && occ > 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march<false, march::F_HEART>, 256, 0) ==
+                hipSuccess &&
+            occ > 0)
             per = occ;
         const char *e = getenv("PT_WF_MARCH_BLOCKS_PER_CU");  // tuning knob
         if (e && atoi(e) > 0 && atoi(e) < per) per = atoi(e);
@@ -714,13 +705,13 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
             if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
-            launch_bounce<NW, true>((paths + 255) / 256, st, sc, P0, v, 0);
+            launch_bounce<NW, true>((paths + 255) / 256, st, sc, P0, v, 0, ws->diag, fkind);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
                     if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
-                    launch_bounce<NW, false>(bb, st, sc, P0, v, it);
+                    launch_bounce<NW, false>(bb, st, sc, P0, v, it, ws->diag, fkind);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
                 }
@@ -734,8 +725,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, st, K_MARCH)) != hipSuccess) return e;
-                if (ws->diag) wf_march<true><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);
-                else wf_march<false><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
+                if (fkind != march::F_HEART) wf_march<false, march::F_ANY><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
+                else if (ws->diag) wf_march<true, march::F_HEART><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);
+                else wf_march<false, march::F_HEART><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
             }
@@ -749,12 +741,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
 }
 
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
-                              WaveWorkspace *ws) {
+                              WaveWorkspace *ws, int fkind) {
     if (P.tile_count == 0 || P.spp == 0) return hipSuccess;
-    if (P.depth <= 8) return render_wave_nw<4>(sc, P, out, st, ws);
-    if (P.depth <= 16) return render_wave_nw<8>(sc, P, out, st, ws);
-    if (P.depth <= 32) return render_wave_nw<16>(sc, P, out, st, ws);
-    return render_wave_nw<32>(sc, P, out, st, ws);
+    // the NW template only sizes the megakernel's register stacks; the
+    // wavefront keeps attenuation ids in HBM, so one build serves every depth
+    return render_wave_nw<4>(sc, P, out, st, ws, fkind);
 }
 
 }  // namespace pt

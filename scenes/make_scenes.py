@@ -8,6 +8,10 @@ arrangement.  The schema is SceneJson (src/world/json_models.rs:23-29).
 
     python scenes/make_scenes.py            # writes cornell_box.json, spheres.json
     python scenes/make_scenes.py --synthetic N   # also synthetic_N.json (config C5)
+
+marched.json exercises every ray-marched ShapeFunction of the reference
+(Heart, Sine, Star, DupinCyclide, HuntsSurface, Cushion;
+src/world/shapes/ray_marching.rs:121-520) on a ground plane under a light.
 """
 import argparse
 import json
@@ -89,6 +93,40 @@ def spheres():
     }
 
 
+def marched():
+    def fn(name, shape, t, r, scale, mat, step=0.01, depth=4):
+        return {"type": "BruteForsableShape", "name": name, "shape": shape, "step": step, "depth": depth,
+                "transform": tr(t, r, (scale, scale, scale)), "material": mat}
+
+    shapes = [
+        {"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+         "material": "Ground"},
+        {"type": "Rectangle", "x0": -3, "x1": 3, "y0": -2, "y1": 2, "transform": tr((0, 9, 2), (90, 0, 0)),
+         "material": "Light"},
+        fn("Dupin", {"type": "DupinCyclide", "a": 1.11, "b": 0.99, "c": 0.5, "d": 0.1, "sphere_radius": 2.5},
+           (-6, 1.6, 0), (0, -100, 0), 1.2, "Copper"),
+        fn("Sine", {"type": "Sine", "a": 1.0, "sphere_radius": 1.5}, (-3, 1.6, 0), (20, 30, 0), 1.0, "Chalk"),
+        fn("Star", {"type": "Star", "a": -1.0, "sphere_radius": 1.6}, (0, 1.6, 0), (0, 45, 10), 1.0, "Glass"),
+        fn("Hunts", {"type": "HuntsSurface", "sphere_radius": 4.0}, (3, 1.6, 0), (-90, 0, 0), 0.35, "Steel"),
+        fn("Cushion", {"type": "Cushion", "sphere_radius": 1.5}, (6, 1.6, 0), (-70, 20, 0), 1.1, "Chalk", depth=3),
+        fn("Heart", {"type": "Heart"}, (0, 1.2, -3), (-90, 0, 0), 0.8, "Copper", step=0.005),
+    ]
+    return {
+        "camera": {"position": [0, 3.5, -16], "direction": [0, -0.12, 1], "up": [0, 1, 0], "fov": 40,
+                   "focal_length": 1},
+        "shapes": shapes,
+        "materials": {
+            "Ground": lambert((0.45, 0.5, 0.45)),
+            "Light": {"type": "DiffuseLight", "emit": solid((6, 6, 6))},
+            "Copper": {"type": "Metal", "albedo": solid((0.8, 0.5, 0.3)), "fuzz": 0.2},
+            "Chalk": lambert((0.8, 0.8, 0.75)),
+            "Glass": {"type": "Dielectric", "index_of_refraction": 1.5},
+            "Steel": {"type": "Metal", "albedo": solid((0.6, 0.6, 0.65)), "fuzz": 0},
+        },
+        "background": [0, 0, 0],
+    }
+
+
 def synthetic(n, seed=1):
     """C5: n small spheres on a jittered grid (add_random_spheres recipe scaled up,
     json_models.rs:73-133), a Lambertian ground sphere and the spheres.json camera."""
@@ -130,6 +168,7 @@ def main():
     a = ap.parse_args()
     (HERE / "cornell_box.json").write_text(json.dumps(cornell(), indent=1) + "\n")
     (HERE / "spheres.json").write_text(json.dumps(spheres(), indent=1) + "\n")
+    (HERE / "marched.json").write_text(json.dumps(marched(), indent=1) + "\n")
     if a.synthetic:
         (HERE / ("synthetic_%d.json" % a.synthetic)).write_text(json.dumps(synthetic(a.synthetic)) + "\n")
 

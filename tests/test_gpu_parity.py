@@ -320,3 +320,39 @@ def test_count_work_matches_host_build(pt, cornell, cornell_text):
     want = (C.c_uint64 * len(pt.COUNTERS))()
     L.h_count_work(h, w, hh, 4, 8, 1, px.ctypes.data_as(C.POINTER(C.c_uint32)), len(px), want)
     assert got == dict(zip(pt.COUNTERS, list(want)))
+
+
+def test_marched_functions_frame_and_hits(pt):
+    """scenes/marched.json: every reference ShapeFunction (Heart, Sine, Star,
+    DupinCyclide, HuntsSurface, Cushion) through the GPU's generic skipping
+    march, both engines, against the oracle's literal march."""
+    from conftest import scene_text
+    text = scene_text("marched.json")
+    ps = pt.Scene.from_json(text, random_spheres=False)
+    osc = O.Scene(text, random_spheres=False)
+    img, ref = render_pair(pt, (ps, osc), 96, 54, 2, 8, seed=3)
+    check_image(img, ref)
+    r = pt.HipRenderer(ps, depth=8)
+    with _env(PT_ENGINE="mega"):
+        mega = r.render(ps.camera(), pt.ImageParams(96, 54), 2, seed=3)
+    assert np.array_equal(mega, img)
+    rng = np.random.default_rng(31)
+    rays = []
+    for i in range(2, 8):
+        m = list(osc.shape(i).direct)
+        c = np.array([m[3], m[7], m[11]])
+        tgt = c + rng.uniform(-2, 2, size=(800, 3))
+        o = np.tile([0.0, 3.5, -16.0], (800, 1))
+        o[400:] = c + rng.uniform(-3, 3, size=(400, 3))
+        d = tgt - o
+        d[400:] = rng.normal(size=(400, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rays.append(np.concatenate([o, d], 1))
+    rays = np.concatenate(rays)
+    got = r.closest_hit(rays)
+    bad = 0
+    for i, ray in enumerate(rays):
+        h = osc.closest_hit(ray[:3], ray[3:])
+        g = got[i]
+        bad += (g["shape"] != -1) if h is None else not (g["shape"] == h.shape and g["t"] == h.t)
+    assert bad == 0, "%d of %d rays differ" % (bad, len(rays))

@@ -60,6 +60,12 @@ static void hook_lv_end() {
 static void hook_block_begin() { g_block_max = 0; }
 static void hook_block_end() { g_hist_blockmax[g_block_max < 63 ? g_block_max : 63]++; }
 
+static march::FParams heartF() {
+    march::FParams F{};
+    F.func = march::F_HEART;
+    return F;
+}
+
 // The reference march, literally (ray_marching.rs:20-74), in object space.
 static bool literal_march(const Job &j, double *t_out, long *steps) {
     double start, end;
@@ -181,7 +187,7 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < n; i++) {
             const Job &q = jobs[i];
             march::MarchState m;
-            march::march_begin(q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m);
+            march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m);
             unsigned long long it0 = g_prof.iters;
             uint32_t tr0 = ms.tries;
             int stt;
@@ -221,7 +227,7 @@ int main(int argc, char **argv) {
                 march::MarchStats st2{0, 0, 0};
                 int stt = march::M_MISS;
                 double k = 0;
-                if (march::march_begin(q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m))
+                if (march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m))
                     while ((stt = march::march_iter<false>(m, &st2)) == march::M_RUNNING) k++;
                 double rec[3] = {m.t, stt == march::M_DONE ? 1.0 : 0.0, k};
                 fwrite(rec, sizeof rec, 1, o);

@@ -201,6 +201,47 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
     }
 }
 
+// Read of scene data at a wave-uniform address: through the constant address
+// space, so the compiler may use scalar loads (the scene is read-only while
+// kernels run; __restrict__ on struct members does not tell it so).
+template <class T>
+PT_HD T uniform_load(const T *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const __attribute__((address_space(4))) T *)p;
+#else
+    return *p;
+#endif
+}
+
+// A shape at a wave-uniform address, all fields but `dir` loaded one by one
+// (an aggregate copy is folded back to the global pointer); the unused ones
+// are dropped by the compiler.
+PT_HD DShape uniform_shape(const DShape *p) {
+    DShape s;
+#pragma unroll
+    for (int k = 0; k < 12; k++) s.inv[k] = uniform_load(&p->inv[k]);
+#pragma unroll
+    for (int k = 0; k < 4; k++) s.p[k] = uniform_load(&p->p[k]);
+    s.type = uniform_load(&p->type);
+    s.material = uniform_load(&p->material);
+    s.depth = uniform_load(&p->depth);
+    s.func = uniform_load(&p->func);
+#pragma unroll
+    for (int k = 0; k < 4; k++) s.fk[k] = uniform_load(&p->fk[k]);
+    s.fradius = uniform_load(&p->fradius);
+    return s;
+}
+
+PT_HD DBox uniform_box(const DBox *p) {
+    DBox b;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        b.lo[k] = uniform_load(&p->lo[k]);
+        b.hi[k] = uniform_load(&p->hi[k]);
+    }
+    return b;
+}
+
 struct Scene {
     const DShape *__restrict__ shapes;
     const DMaterial *__restrict__ mats;
@@ -235,9 +276,10 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     int who = *who_out;
     // wave-uniform list (few JSON shapes): scalar loads of each shape
     for (int k = 0; k < sc.nlin; k++) {
-        int i = sc.lin[k];
+        const int i = uniform_load(&sc.lin[k]);
+        const DShape s = uniform_shape(&sc.shapes[i]);
         double t;
-        if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+        if (shape_test<STATS, march::F_ANY, false>(s, r, min_t, best, &t, ct) && (t < best || i > who)) {
             best = t;
             who = i;
         }

@@ -169,10 +169,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             // does any marched shape's bound start before the best hit? (the
             // march kernel repeats this select and marches)
             for (int k = 0; k < sc.nmarch && !need_march; k++) {
-                const int s = sc.march[k];
-                const DBox &b = sc.boxes[s];
+                const int s = dev::uniform_load(&sc.march[k]);
+                const DBox b = dev::uniform_box(&sc.boxes[s]);
                 if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
-                const DShape &S = sc.shapes[s];
+                const DShape S = dev::uniform_shape(&sc.shapes[s]);
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
@@ -584,7 +584,10 @@ void wave_workspace_free(WaveWorkspace *ws) {
 
 static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
     if (bytes <= ws->bytes) return hipSuccess;
-    wave_workspace_free(ws);
+    // grow the path storage only; an enabled timer or diag buffer stays
+    if (ws->base) (void)hipFree(ws->base);
+    ws->base = nullptr;
+    ws->bytes = 0;
     hipError_t e = hipMalloc(&ws->base, bytes);
     if (e != hipSuccess) {
         ws->base = nullptr;
@@ -597,7 +600,7 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
 static int bounce_waves() {
     const char *e = getenv("PT_WF_BOUNCE_WAVES");
     const int w = e ? atoi(e) : PT_WF_BOUNCE_WAVES;
-    return w >= 2 && w <= 4 ? w : PT_WF_BOUNCE_WAVES;
+    return w >= 2 && w <= 8 ? w : PT_WF_BOUNCE_WAVES;
 }
 
 template <int NW, bool FIRST>
@@ -618,6 +621,9 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
     switch (bounce_waves()) {
     case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 5: wf_bounce<NW, FIRST, 5, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 6: wf_bounce<NW, FIRST, 6, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 8: wf_bounce<NW, FIRST, 8, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     default: wf_bounce<NW, FIRST, 3, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     }
 }

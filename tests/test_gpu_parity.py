@@ -356,3 +356,17 @@ def test_marched_functions_frame_and_hits(pt):
         g = got[i]
         bad += (g["shape"] != -1) if h is None else not (g["shape"] == h.shape and g["t"] == h.t)
     assert bad == 0, "%d of %d rays differ" % (bad, len(rays))
+
+
+def test_kernel_timing_from_first_frame(pt, cornell):
+    """Timing enabled on a fresh renderer (before its workspace exists) covers
+    the first frame; timing and the image do not depend on each other."""
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam, ip = ps.camera(), pt.ImageParams(48, 32)
+    pt.kernel_timing(r, True)
+    img = r.render(cam, ip, 2, seed=4)
+    kt = pt.kernel_timing(r, False)
+    assert kt["bounce"][1] > 0 and kt["bounce"][0] > 0.0
+    assert kt["march"][1] > 0 and kt["select"][1] > 0 and kt["reduce"][1] > 0
+    assert np.array_equal(img, r.render(cam, ip, 2, seed=4))

@@ -34,6 +34,12 @@ struct WaveWorkspace {
     size_t bytes = 0;
     unsigned long long *diag = nullptr;  // march-kernel phase diagnostics (pt_wave_diag), when enabled
     KernelTimer *timer = nullptr;         // per-kernel timing (pt_kernel_timing), when enabled
+    // chunk pipeline: extra launch streams (chunk c runs on stream c % slots,
+    // stream 0 being the caller's) and the events that order them
+    static constexpr int MAX_SLOTS = 4;
+    hipStream_t side[MAX_SLOTS - 1] = {};
+    hipEvent_t fork = nullptr, join[MAX_SLOTS - 1] = {}, reduced = nullptr;
+    int device = -1;
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

@@ -305,9 +305,6 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_VOTE
 #define PT_WF_VOTE 0
 #endif
-#ifndef PT_WF_PREFETCH
-#define PT_WF_PREFETCH 0
-#endif
 #ifndef PT_WF_SEL_BATCH
 #define PT_WF_SEL_BATCH 0
 #endif
@@ -336,28 +333,39 @@ __device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob 
 // 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
 template <bool DIAG, int FK = march::F_ANY>
-__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag) {
+__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag,
+                                                                            uint32_t slice) {
     __shared__ uint32_t head;
     const int nm = sc.nmarch;
     const uint32_t count = v.cnt[it * 4 + 1];
     const uint32_t *mq = v.mq;
-    const uint32_t per = (count + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = blockIdx.x * per, hi = min(count, lo + per);
-    if (threadIdx.x == 0) head = lo + blockDim.x;
+    // The block's jobs: local index q = 0, 1, ... maps to the queue position
+    // pos(q).  slice == 0: one contiguous slice of the queue per block.
+    // slice > 0: runs of `slice` consecutive jobs dealt round-robin to the
+    // blocks, so a heavy region of the (pixel-sorted) queue is shared by many
+    // blocks while each run stays pixel-coherent.
+    uint32_t per, lo;
+    if (slice == 0) {
+        per = (count + gridDim.x - 1) / gridDim.x;
+        lo = blockIdx.x * per;
+    } else {
+        const uint32_t runs = (count + slice - 1) / slice;
+        const uint32_t mine = runs > blockIdx.x ? (runs - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
+        per = mine * slice;
+        lo = 0;
+    }
+    const uint32_t G = gridDim.x;
+    auto pos = [&](uint32_t q) -> uint32_t {
+        return slice == 0 ? lo + q : (q / slice * G + blockIdx.x) * slice + q % slice;
+    };
+    const uint32_t hi = slice == 0 ? min(count, lo + per) : per;
+    if (slice == 0) per = hi > lo ? hi - lo : 0u;
+    if (threadIdx.x == 0) head = blockDim.x;
     __syncthreads();
-    uint32_t q = lo + threadIdx.x;
-    bool have = q < hi;
+    uint32_t q = threadIdx.x;
+    bool have = q < per && pos(q) < count;
     MarchJob cur;
-    if (have) load_job(v, mq[q], &cur);
-#if PT_WF_PREFETCH
-    // next job's state in flight, the index after it
-    MarchJob nxt;
-    uint32_t qn = have ? atomicAdd(&head, 1u) : hi;
-    bool nhave = qn < hi;
-    if (nhave) load_job(v, mq[qn], &nxt);
-    uint32_t q2 = nhave ? atomicAdd(&head, 1u) : hi;
-    uint32_t id2 = q2 < hi ? mq[q2] : 0u;
-#endif
+    if (have) load_job(v, mq[pos(q)], &cur);
     bool marching = false;
     int km = 0, mshape = -1;
     V3 inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
@@ -443,20 +451,9 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             if (done) {
                 v.t[cur.id] = cur.best;
                 v.who[cur.id] = cur.who;
-#if PT_WF_PREFETCH
-                have = nhave;
-                if (have) {
-                    cur = nxt;
-                    nhave = q2 < hi;
-                    if (nhave) load_job(v, id2, &nxt);
-                    q2 = nhave ? atomicAdd(&head, 1u) : hi;
-                    id2 = q2 < hi ? mq[q2] : 0u;
-                }
-#else
                 q = atomicAdd(&head, 1u);
-                have = q < hi;
-                if (have) load_job(v, mq[q], &cur);
-#endif
+                have = q < per && pos(q) < count;
+                if (have) load_job(v, mq[pos(q)], &cur);
                 if (have) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
@@ -564,8 +561,6 @@ hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches) {
 }
 
 // ------------------------------------------------------------- host driver
-static size_t path_bytes(uint32_t depth) { return 7 * 8 + 8 + 4 + 4 + (size_t)(depth + 1) * 4 + 3 * 8 + 2 * 4 + 1; }
-
 static uint32_t wf_cap_paths() {
     const char *e = getenv("PT_WF_PATHS");
     long v = e ? atol(e) : (1l << 24);
@@ -573,6 +568,15 @@ static uint32_t wf_cap_paths() {
 }
 
 void wave_workspace_free(WaveWorkspace *ws) {
+    for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
+        if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
+        if (ws->join[k]) (void)hipEventDestroy(ws->join[k]);
+        ws->side[k] = nullptr;
+        ws->join[k] = nullptr;
+    }
+    if (ws->fork) (void)hipEventDestroy(ws->fork);
+    if (ws->reduced) (void)hipEventDestroy(ws->reduced);
+    ws->fork = ws->reduced = nullptr;
     timer_free(ws->timer);
     ws->timer = nullptr;
     if (ws->diag) (void)hipFree(ws->diag);
@@ -628,6 +632,46 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
     }
 }
 
+// Chunks in flight: each has its own path state (slot) and runs on its own
+// stream, so one chunk's bounce/compaction kernels fill the tails of the
+// other's march kernels (and its memory-bound bounces overlap the other's
+// VALU-bound marches).  Only the reduces are chained, in chunk order.
+static int pipeline_slots() {
+    const char *e = getenv("PT_WF_SLOTS");
+    const int k = e ? atoi(e) : 2;
+    return k < 1 ? 1 : (k > WaveWorkspace::MAX_SLOTS ? WaveWorkspace::MAX_SLOTS : k);
+}
+
+static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (ws->device != dev) {  // streams and events belong to one device
+        for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
+            if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
+            if (ws->join[k]) (void)hipEventDestroy(ws->join[k]);
+            ws->side[k] = nullptr;
+            ws->join[k] = nullptr;
+        }
+        if (ws->fork) (void)hipEventDestroy(ws->fork);
+        if (ws->reduced) (void)hipEventDestroy(ws->reduced);
+        ws->fork = ws->reduced = nullptr;
+        ws->device = dev;
+    }
+    if (!ws->fork && (e = hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
+    for (int k = 0; k < slots - 1; k++) {
+        if (!ws->side[k] && (e = hipStreamCreateWithFlags(&ws->side[k], hipStreamNonBlocking)) != hipSuccess) return e;
+        if (!ws->join[k] && (e = hipEventCreateWithFlags(&ws->join[k], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+struct Slot {
+    WfView v;
+    uint32_t *cp_blk;
+};
+
 template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws, int fkind) {
@@ -644,38 +688,51 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
     const size_t cnt_words = (size_t)(iters + 2) * 4;
     const uint32_t cap_tiles = (cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
-    const size_t bytes = (size_t)cap * path_bytes(P0.depth) + (size_t)cap_tiles * CP_TILE + (size_t)cap_tiles * 8 +
-                         (size_t)npix_max * 24 + cnt_words * 4 + 8192;
-    hipError_t e = reserve(ws, bytes);
+    // no more slots than chunks
+    const uint64_t chunks = (uint64_t)((ntiles + group_tiles - 1) / group_tiles) * ((P0.spp + ns - 1) / ns);
+    int slots = pipeline_slots();
+    if ((uint64_t)slots > chunks) slots = (int)chunks;
+    hipError_t e = ensure_streams(ws, slots);
     if (e != hipSuccess) return e;
-    // carve the workspace
+    auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+    const size_t slot_bytes = al((size_t)cap * 8) * 11 + al((size_t)cap * 4) * 4 + al((size_t)cap * 4 * (P0.depth + 1)) +
+                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 8) + al(cnt_words * 4);
+    const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
+    e = reserve(ws, bytes);
+    if (e != hipSuccess) return e;
+    // carve the workspace: the slots' path state, then the shared running sums
     char *p = (char *)ws->base;
     auto take = [&](size_t n) {
         char *r = p;
-        p += (n + 255) & ~(size_t)255;
+        p += al(n);
         return (void *)r;
     };
-    WfView v;
-    v.ox = (double *)take((size_t)cap * 8);
-    v.oy = (double *)take((size_t)cap * 8);
-    v.oz = (double *)take((size_t)cap * 8);
-    v.dx = (double *)take((size_t)cap * 8);
-    v.dy = (double *)take((size_t)cap * 8);
-    v.dz = (double *)take((size_t)cap * 8);
-    v.t = (double *)take((size_t)cap * 8);
-    v.rng = (uint64_t *)take((size_t)cap * 8);
-    v.who = (int32_t *)take((size_t)cap * 4);
-    v.meta = (uint32_t *)take((size_t)cap * 4);
-    v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
-    v.rx = (double *)take((size_t)cap * 8);
-    v.ry = (double *)take((size_t)cap * 8);
-    v.rz = (double *)take((size_t)cap * 8);
-    v.list = (uint32_t *)take((size_t)cap * 4);
-    v.mq = (uint32_t *)take((size_t)cap * 4);
-    v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
-    uint32_t *cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
-    v.acc = (double *)take((size_t)npix_max * 24);
-    v.cnt = (uint32_t *)take(cnt_words * 4);
+    Slot sl[WaveWorkspace::MAX_SLOTS];
+    for (int k = 0; k < slots; k++) {
+        WfView &v = sl[k].v;
+        v.ox = (double *)take((size_t)cap * 8);
+        v.oy = (double *)take((size_t)cap * 8);
+        v.oz = (double *)take((size_t)cap * 8);
+        v.dx = (double *)take((size_t)cap * 8);
+        v.dy = (double *)take((size_t)cap * 8);
+        v.dz = (double *)take((size_t)cap * 8);
+        v.t = (double *)take((size_t)cap * 8);
+        v.rng = (uint64_t *)take((size_t)cap * 8);
+        v.who = (int32_t *)take((size_t)cap * 4);
+        v.meta = (uint32_t *)take((size_t)cap * 4);
+        v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
+        v.rx = (double *)take((size_t)cap * 8);
+        v.ry = (double *)take((size_t)cap * 8);
+        v.rz = (double *)take((size_t)cap * 8);
+        v.list = (uint32_t *)take((size_t)cap * 4);
+        v.mq = (uint32_t *)take((size_t)cap * 4);
+        v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
+        sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
+        v.cnt = (uint32_t *)take(cnt_words * 4);
+        v.cap = cap;
+    }
+    double *acc = (double *)take((size_t)npix_max * 24);
+    for (int k = 0; k < slots; k++) sl[k].v.acc = acc;
     if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
 
     // persistent march grid: exactly the resident blocks of the device
@@ -694,54 +751,79 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         if (e && atoi(e) > 0 && atoi(e) < per) per = atoi(e);
         return (uint32_t)(cus * per);
     }();
+    static uint32_t march_slice = [] {
+        const char *e = getenv("PT_WF_MARCH_SLICE");  // tuning knob: 0 = one contiguous slice per block (measured: 256 is 7 % faster)
+        return e ? (uint32_t)atoi(e) : 256u;
+    }();
+    // the side streams start after everything the caller queued on st
+    if (slots > 1) {
+        if ((e = hipEventRecord(ws->fork, st)) != hipSuccess) return e;
+        for (int k = 0; k < slots - 1; k++)
+            if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
+    }
+    uint64_t c = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        v.tile0 = P0.tile_begin + g0;
-        v.npix = gt * TILE * TILE;
-        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns) {
+        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns, c++) {
+            const int k = (int)(c % (uint64_t)slots);
+            const hipStream_t cs = k == 0 ? st : ws->side[k - 1];
+            WfView &v = sl[k].v;
+            uint32_t *cp_blk = sl[k].cp_blk;
+            v.tile0 = P0.tile_begin + g0;
+            v.npix = gt * TILE * TILE;
             v.s0 = s0;
             v.ns = P0.spp - s0 < ns ? P0.spp - s0 : ns;
-            v.cap = cap;
             const uint32_t paths = v.ns * v.npix;
-            e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, st);
+            e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs);
             if (e != hipSuccess) return e;
-            e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, st);
+            e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, cs);
             if (e != hipSuccess) return e;
             uint32_t bb = (paths + 255) / 256;
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
-            if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
-            launch_bounce<NW, true>((paths + 255) / 256, st, sc, P0, v, 0, ws->diag, fkind);
+            if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
+            launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
+            if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
-                    if ((e = timer_begin(ws->timer, st, K_BOUNCE)) != hipSuccess) return e;
-                    launch_bounce<NW, false>(bb, st, sc, P0, v, it, ws->diag, fkind);
+                    if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
+                    launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
-                    if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
+                    if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 }
                 if (it == iters - 1) break;  // the last bounce only shades
                 // live list for it + 1 and march queue for it, both id-sorted
-                if ((e = timer_begin(ws->timer, st, K_SELECT)) != hipSuccess) return e;
+                if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
-                cp_count<<<ptiles, CP_BLOCK, 0, st>>>(v.status, cp_blk);
-                cp_scan<<<1, CP_BLOCK, 0, st>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1]);
-                cp_scatter<<<ptiles, CP_BLOCK, 0, st>>>(v.status, cp_blk, v.list, v.mq);
+                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk);
+                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1]);
+                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, v.list, v.mq);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
-                if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
-                if ((e = timer_begin(ws->timer, st, K_MARCH)) != hipSuccess) return e;
-                if (fkind != march::F_HEART) wf_march<false, march::F_ANY><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
-                else if (ws->diag) wf_march<true, march::F_HEART><<<march_blocks, 256, 0, st>>>(sc, v, it, ws->diag);
-                else wf_march<false, march::F_HEART><<<march_blocks, 256, 0, st>>>(sc, v, it, nullptr);
+                if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
+                if (fkind != march::F_HEART)
+                    wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
+                else if (ws->diag)
+                    wf_march<true, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, ws->diag, march_slice);
+                else
+                    wf_march<false, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
-                if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
+                if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             }
-            if ((e = timer_begin(ws->timer, st, K_REDUCE)) != hipSuccess) return e;
-            wf_reduce<<<(v.npix + 255) / 256, 256, 0, st>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+            // the per-pixel sums take the chunks in order
+            if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
+            if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
+            wf_reduce<<<(v.npix + 255) / 256, 256, 0, cs>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = timer_end(ws->timer, st)) != hipSuccess) return e;
+            if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+            if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;
         }
+    }
+    // the caller's stream resumes after every side stream's last chunk
+    for (int k = 0; k < slots - 1; k++) {
+        if ((e = hipEventRecord(ws->join[k], ws->side[k])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st, ws->join[k], 0)) != hipSuccess) return e;
     }
     return hipSuccess;
 }

@@ -1,0 +1,16 @@
+# Evidence run on one MI355X: GPU tests, smoke, default bench, rocprofv3
+# kernel stats of the same bench command, PMC FETCH/WRITE passes (separate runs).
+# usage: bash scripts/gpu_evidence.sh <tag>
+set -e
+TAG=${1:-r1}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+timeout -k 10 400 python bench.py > $OUT/bench_default.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline > $OUT/kt_bench.log 2>&1
+B="python3 $GRAFT_REPO_ROOT/bench.py --spp 8 --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/pmc_fetch -o p --pmc FETCH_SIZE -- $B > $OUT/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/pmc_write -o p --pmc WRITE_SIZE -- $B > $OUT/pmc_write.log 2>&1

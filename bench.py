@@ -215,7 +215,11 @@ def main():
                          "flops_per_sample_total": round(F, 1),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},
-                         "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3)},
+                         "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3),
+                         # two chunks run concurrently (pt_wave.hip), so one kernel's launches overlap the
+                         # other kind's: the whole path's rate is the frame's FLOPs over the frame time
+                         "path_achieved": round(F * value * 1e6 / 1e12, 4),
+                         "path_frac": round(F * value * 1e6 / 1e12 / FP64_PEAK_TFLOPS, 5)},
             "roofline_hbm": {"achieved": round(out_bytes / (kernel_ms / 1e3) / 1e9, 4), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},

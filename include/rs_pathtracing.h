@@ -56,10 +56,21 @@ typedef struct pt_renderer pt_renderer;
 /* Scene::from_json options.  The reference appends ~480 spheres drawn from an
  * unseeded thread_rng (src/world/json_models.rs:44, 50-133); here the draw is
  * seeded so a scene is reproducible, and it can be switched off. */
+/* ImageTexture decoding: the reference calls image::open(image_filename) and
+ * into_rgba8() at deserialization (src/world/texture.rs:119-130).  A loader
+ * returns PT_OK with a width x height RGBA8 row-major buffer that stays valid
+ * until pt_scene_create_from_json returns (the library copies it), or
+ * PT_ERR_UNSUPPORTED to decline the file.  Without a loader, or for a
+ * declined file, the built-in reader takes binary PPM (P6, maxval 255). */
+typedef int (*pt_image_loader)(void *user, const char *filename, uint32_t *width, uint32_t *height,
+                               const uint8_t **rgba8);
+
 typedef struct {
     uint32_t random_spheres; /* 1 = reference behaviour (default), 0 = JSON shapes only */
     uint32_t reserved;
-    uint64_t seed; /* seed of the add_random_spheres stream */
+    uint64_t seed; /* seed of the add_random_spheres stream and of the NoiseTexture Perlin tables */
+    pt_image_loader load_image; /* NULL: built-in PPM reader */
+    void *image_user;
 } pt_scene_opts;
 
 /* Camera (src/camera/mod.rs:36-46).  fov in radians, as Camera::new takes it. */
@@ -77,7 +88,8 @@ typedef struct {
 } pt_shape_info;
 
 typedef struct {
-    int32_t type, pad0;
+    int32_t type;
+    int32_t texture; /* -1: SolidColor (albedo / emit hold it); else the root of a non-solid texture */
     double albedo[3];
     double fuzz, ior;
     double emit[3];
@@ -125,7 +137,8 @@ int pt_render_stop(pt_renderer *r);
 
 /* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */
 /* Renders this rank's share of the frame straight into device memory on
- * `hip_stream` (0 = the renderer's stream).  Pixels are cut into 16x16 tiles
+ * `hip_stream` (a hipStream_t; 0 = the null stream, as in every HIP call and
+ * in pt_unshard_device).  Pixels are cut into 16x16 tiles
  * numbered row-major; tile k belongs to rank k % world.  world == 1: d_out is
  * the w*h*3 frame.  world > 1: d_out holds this rank's tiles in order,
  * pt_shard_tiles(...) * 256 * 3 doubles (pixels outside the frame are 0). */

@@ -38,8 +38,16 @@ class ShapeIn(C.Structure):
 
 
 class MaterialIn(C.Structure):
-    _fields_ = [("type", C.c_int32), ("pad0", C.c_int32), ("albedo", C.c_double * 3),
+    _fields_ = [("type", C.c_int32), ("tex", C.c_int32), ("albedo", C.c_double * 3),
                 ("fuzz", C.c_double), ("ior", C.c_double), ("emit", C.c_double * 3)]
+
+
+TEX_SOLID, TEX_CHECKER, TEX_UVCHECKER, TEX_NOISE, TEX_IMAGE = 0, 1, 2, 3, 4
+
+
+class TextureIn(C.Structure):
+    _fields_ = [("type", C.c_int32), ("odd", C.c_int32), ("even", C.c_int32), ("aux", C.c_int32),
+                ("c", C.c_double * 3)]
 
 
 class ShapeOut(C.Structure):
@@ -54,7 +62,7 @@ class ShapeOut(C.Structure):
 class Hit(C.Structure):
     _fields_ = [("t", C.c_double), ("point", C.c_double * 3), ("normal", C.c_double * 3),
                 ("front_face", C.c_int32), ("shape", C.c_int32), ("material", C.c_int32),
-                ("pad0", C.c_int32)]
+                ("pad0", C.c_int32), ("u", C.c_double), ("v", C.c_double)]
 
 
 class Stats(C.Structure):
@@ -100,6 +108,13 @@ def lib():
     L.or_scene_new.argtypes = [C.POINTER(ShapeIn), C.c_int, C.POINTER(MaterialIn), C.c_int, C.c_int,
                                C.c_uint64]
     L.or_scene_free.argtypes = [C.c_void_p]
+    L.or_scene_set_textures.argtypes = [C.c_void_p, C.POINTER(TextureIn), C.c_int, C.c_uint64]
+    L.or_scene_add_image.restype = C.c_int
+    L.or_scene_add_image.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]
+    L.or_perlin_tables.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_int32), d3]
+    L.or_perlin_turb.restype = C.c_double
+    L.or_perlin_turb.argtypes = [C.c_uint64, C.c_uint32, d3]
+    L.or_texture_value.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, d3, d3]
     L.or_scene_num_shapes.argtypes = [C.c_void_p]
     L.or_scene_num_materials.argtypes = [C.c_void_p]
     L.or_scene_get_shape.argtypes = [C.c_void_p, C.c_int, C.POINTER(ShapeOut)]
@@ -152,38 +167,101 @@ def vec3(v):
     return [float(x) for x in v]
 
 
-def _texture_color(tex):
-    if tex.get("type") != "SolidColor":
-        raise NotImplementedError("oracle supports SolidColor textures only: %r" % tex.get("type"))
-    return vec3(tex["color"])
+def read_ppm(path):
+    """Binary PPM (P6, maxval 255) -> (width, height, RGBA8 bytes), alpha 255."""
+    data = Path(path).read_bytes()
+    fields, pos = [], 0
+    while len(fields) < 4:
+        while data[pos:pos + 1].isspace():
+            pos += 1
+        if data[pos:pos + 1] == b"#":
+            pos = data.index(b"\n", pos) + 1
+            continue
+        end = pos
+        while not data[end:end + 1].isspace():
+            end += 1
+        fields.append(data[pos:end])
+        pos = end
+    pos += 1  # the single whitespace byte after maxval
+    if fields[0] != b"P6" or fields[3] != b"255":
+        raise ValueError("not a P6/255 PPM: %s" % path)
+    w, h = int(fields[1]), int(fields[2])
+    rgb = np.frombuffer(data, np.uint8, w * h * 3, pos).reshape(-1, 3)
+    rgba = np.concatenate([rgb, np.full((w * h, 1), 255, np.uint8)], axis=1)
+    return w, h, rgba.tobytes()
 
 
-def records_from_json(text: str):
-    """Scene JSON -> (shape records, material records, camera dict).
+class _Textures:
+    """Texture trees (src/world/texture.rs) flattened in pre-order: a node,
+    then its odd subtree, then its even one.  SolidColor at a material's root
+    stays inline (tex = -1)."""
+
+    def __init__(self, images):
+        self.nodes, self.image_list, self.images = [], [], images or {}
+
+    def node(self, tex):
+        t = tex["type"]
+        i = len(self.nodes)
+        rec = {"type": None, "odd": -1, "even": -1, "aux": -1, "c": [0.0, 0.0, 0.0]}
+        self.nodes.append(rec)
+        if t == "SolidColor":
+            rec["type"], rec["c"] = TEX_SOLID, vec3(tex["color"])
+        elif t == "CheckerTexture":
+            rec["type"], rec["c"] = TEX_CHECKER, vec3(tex["multipliers"])
+            rec["odd"] = self.node(tex["odd"])
+            rec["even"] = self.node(tex["even"])
+        elif t == "UVChecker":
+            m = tex["multipliers"]
+            rec["type"], rec["c"] = TEX_UVCHECKER, [float(m[0]), float(m[1]), 0.0]
+            rec["odd"] = self.node(tex["odd"])
+            rec["even"] = self.node(tex["even"])
+        elif t == "NoiseTexture":
+            rec["type"], rec["c"] = TEX_NOISE, [float(tex["scale"]), 0.0, 0.0]
+        elif t == "ImageTexture":
+            fn = tex["image_filename"]
+            rec["type"], rec["aux"] = TEX_IMAGE, len(self.image_list)
+            self.image_list.append(self.images[fn] if fn in self.images else read_ppm(fn))
+        else:
+            raise NotImplementedError(t)
+        return i
+
+    def root(self, tex):
+        """(tex index or -1, solid colour)"""
+        if tex["type"] == "SolidColor":
+            return -1, vec3(tex["color"])
+        return self.node(tex), [0.0, 0.0, 0.0]
+
+
+def records_from_json(text: str, images=None):
+    """Scene JSON -> (shape records, material records, camera dict, textures).
 
     Follows SceneJson (json_models.rs:23-29): materials map (name -> typetag
-    "type"), shapes in file order, camera with fov in degrees.
+    "type"), shapes in file order, camera with fov in degrees.  images maps
+    ImageTexture file names to (width, height, RGBA8 bytes); other files are
+    read as binary PPM.
     """
     js = json.loads(text)
     names = list(js["materials"].keys())
     index = {n: i for i, n in enumerate(names)}
     mats = (MaterialIn * max(1, len(names)))()
+    tx = _Textures(images)
     for i, n in enumerate(names):
         m = js["materials"][n]
         t = m["type"]
+        mats[i].tex = -1
         if t == "Lambertian":
             mats[i].type = LAMBERTIAN
-            mats[i].albedo[:] = _texture_color(m["albedo"])
+            mats[i].tex, mats[i].albedo[:] = tx.root(m["albedo"])
         elif t == "Metal":
             mats[i].type = METAL
-            mats[i].albedo[:] = _texture_color(m["albedo"])
+            mats[i].tex, mats[i].albedo[:] = tx.root(m["albedo"])
             mats[i].fuzz = float(m["fuzz"])
         elif t == "Dielectric":
             mats[i].type = DIELECTRIC
             mats[i].ior = float(m["index_of_refraction"])
         elif t == "DiffuseLight":
             mats[i].type = DIFFUSE_LIGHT
-            mats[i].emit[:] = _texture_color(m["emit"])
+            mats[i].tex, mats[i].emit[:] = tx.root(m["emit"])
         elif t == "EmptyMaterial":
             mats[i].type = EMPTY
         else:
@@ -224,15 +302,24 @@ def records_from_json(text: str):
     camera = {"position": vec3(cam["position"]), "direction": vec3(cam["direction"]),
               "up": vec3(cam["up"]), "fov_deg": float(cam["fov"]),
               "focal_length": float(cam["focal_length"])}
-    return recs, len(shapes), mats, len(names), camera
+    return recs, len(shapes), mats, len(names), camera, tx
 
 
 class Scene:
-    def __init__(self, json_text: str, random_spheres: bool = True, seed: int = 1):
+    def __init__(self, json_text: str, random_spheres: bool = True, seed: int = 1, images=None):
         L = lib()
-        recs, n, mats, nm, cam = records_from_json(json_text)
+        recs, n, mats, nm, cam, tx = records_from_json(json_text, images)
         self._keep = (recs, mats)
         self.ptr = L.or_scene_new(recs, n, mats, nm, 1 if random_spheres else 0, seed)
+        if tx.nodes:
+            arr = (TextureIn * len(tx.nodes))()
+            for i, r in enumerate(tx.nodes):
+                arr[i].type, arr[i].odd, arr[i].even, arr[i].aux = r["type"], r["odd"], r["even"], r["aux"]
+                arr[i].c[:] = r["c"]
+            L.or_scene_set_textures(self.ptr, arr, len(tx.nodes), seed)
+            for w, h, rgba in tx.image_list:
+                buf = (C.c_uint8 * len(rgba)).from_buffer_copy(rgba)
+                L.or_scene_add_image(self.ptr, w, h, buf)
         self.camera_json = cam
         self.n_json_shapes = n
 
@@ -286,6 +373,11 @@ class Scene:
         h = Hit()
         ok = lib().or_shape_hit(self.ptr, i, _d3(o), _d3(d), min_t, max_t, C.byref(h))
         return h if ok else None
+
+    def texture_value(self, tex, u, v, p):
+        out = (C.c_double * 3)()
+        lib().or_texture_value(self.ptr, tex, u, v, _d3(p), out)
+        return np.array(out[:])
 
     def ray_color(self, o, d, depth, rng_state: int):
         st = C.c_uint64(rng_state)

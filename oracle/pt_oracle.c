@@ -283,10 +283,21 @@ typedef struct {
 
 typedef struct {
     int type;
+    int tex; /* -1: SolidColor (albedo / emit) */
     v3 albedo;
     double fuzz, ior;
     v3 emit;
 } mat_t;
+
+typedef struct { /* Perlin (src/algebra/noise.rs:6-16) */
+    int perm_x[256], perm_y[256], perm_z[256];
+    v3 ranvec[256];
+} perlin_t;
+
+typedef struct {
+    uint32_t w, h;
+    uint8_t *rgba;
+} image_t;
 
 typedef struct {
     v3 mn, mx;   /* AABB (src/world/shapes/mod.rs:17-21) */
@@ -302,6 +313,11 @@ struct or_scene {
     bvh_node *nodes;
     int nnodes, root;
     int use_bvh;
+    or_texture_in *tex;
+    int ntex;
+    perlin_t *perlin; /* per texture node (NoiseTexture nodes only) */
+    image_t *images;
+    int nimages;
 };
 
 static int push_mat(or_scene *s, mat_t m) {
@@ -336,6 +352,7 @@ static void add_random_spheres(or_scene *s, uint64_t seed) {
                 double choice = gen_f64_scene(&st);
                 mat_t m;
                 memset(&m, 0, sizeof m);
+                m.tex = -1;
                 if (choice < 0.8) {
                     double rx = uniform_sample(&st, 0.0, s01);
                     double ry = uniform_sample(&st, 0.0, s01);
@@ -370,6 +387,7 @@ or_scene *or_scene_new(const or_shape_in *shapes, int n, const or_material_in *m
     for (int i = 0; i < nm; i++) {
         mat_t m;
         m.type = mats[i].type;
+        m.tex = mats[i].tex;
         m.albedo = vload(mats[i].albedo);
         m.fuzz = mats[i].fuzz;
         m.ior = mats[i].ior;
@@ -403,6 +421,10 @@ or_scene *or_scene_new(const or_shape_in *shapes, int n, const or_material_in *m
 }
 void or_scene_free(or_scene *s) {
     if (!s) return;
+    for (int i = 0; i < s->nimages; i++) free(s->images[i].rgba);
+    free(s->images);
+    free(s->tex);
+    free(s->perlin);
     free(s->nodes);
     free(s->shapes);
     free(s->mats);
@@ -435,6 +457,7 @@ void or_scene_get_material(const or_scene *s, int i, or_material_in *o) {
     const mat_t *m = &s->mats[i];
     memset(o, 0, sizeof *o);
     o->type = m->type;
+    o->tex = m->tex;
     vstore(o->albedo, m->albedo);
     o->fuzz = m->fuzz;
     o->ior = m->ior;
@@ -741,6 +764,44 @@ static v3 shape_obj_normal(const shape_t *s, v3 o, v3 d, double t, v3 *p_out) {
     return V(NAN, NAN, NAN);
 }
 
+/* RayHit u, v from the object-space point, as each ray_intersect builds it:
+ * Sphere mod.rs:361-373 (theta = acos(-p.y), phi = atan2(-p.z, p.x) + PI),
+ * Rectangle :189-190, Cube :267-281 (by the face of the largest |p| component),
+ * ray-marched ShapeFunction::uv (Heart :170, Sine :239, Star :302 -> (0, 0);
+ * DupinCyclide :371, HuntsSurface :436, Cushion :506 -> (p.x, p.y)). */
+static void shape_uv(const shape_t *s, v3 p, double *u, double *v) {
+    switch (s->type) {
+    case OR_SPHERE: {
+        double theta = acos(-p.y);
+        double phi = atan2(-p.z, p.x) + M_PI;
+        *u = phi / (2.0 * M_PI);
+        *v = theta / M_PI;
+        return;
+    }
+    case OR_RECT:
+        *u = (p.x - s->x0) / (s->x1 - s->x0);
+        *v = (p.y - s->y0) / (s->y1 - s->y0);
+        return;
+    case OR_CUBE: {
+        v3 pa = V(fabs(p.x), fabs(p.y), fabs(p.z));
+        double mc = vmaxc(pa);
+        if (mc == pa.x) { *u = p.y; *v = p.z; }
+        else if (mc == pa.y) { *u = p.x; *v = p.z; }
+        else if (mc == pa.z) { *u = p.x; *v = p.y; }
+        else { *u = NAN; *v = NAN; }
+        return;
+    }
+    default:
+        if (s->func == OR_FUNC_DUPIN || s->func == OR_FUNC_HUNTS || s->func == OR_FUNC_CUSHION) {
+            *u = p.x;
+            *v = p.y;
+        } else {
+            *u = 0.0;
+            *v = 0.0;
+        }
+    }
+}
+
 /* Shape::ray_hit_transformed: src/world/shapes/mod.rs:112-124, with
  * RayHit::new (ray.rs:32-52, normal normalised) and set_normal (ray.rs:60-64). */
 static void finish_hit(const shape_t *s, int idx, v3 wo, v3 wd, double t, or_hit *h) {
@@ -752,6 +813,7 @@ static void finish_hit(const shape_t *s, int idx, v3 wo, v3 wd, double t, or_hit
     int front = vdot(n, wd) < 0.0;
     v3 nn = vnorm(front ? n : vneg(n));
     v3 p = mpoint(&s->direct, p_obj);
+    shape_uv(s, p_obj, &h->u, &h->v);
     h->t = t;
     vstore(h->point, p);
     vstore(h->normal, nn);
@@ -942,6 +1004,162 @@ int or_closest_hit(const or_scene *sc, const double o[3], const double d[3], dou
 }
 
 /* ======================================================================= */
+/* Textures (src/world/texture.rs) and Perlin noise (src/algebra/noise.rs)  */
+/* ======================================================================= */
+/* Rng::gen::<u32> on the stream: the high half of the next output (RNG spec). */
+static uint32_t rng_u32(uint64_t *st) { return (uint32_t)(or_rng_next(st) >> 32); }
+/* gen_range(0..n) for u32 = UniformInt::sample_single_inclusive(0, n - 1)
+ * (rand 0.8.5 distributions/uniform.rs): zone = (n << lz(n)) - 1, accept the
+ * high word of v * n when the low word <= zone. */
+static uint32_t rng_below(uint64_t *st, uint32_t n) {
+    uint32_t zone = (n << __builtin_clz(n)) - 1u;
+    for (;;) {
+        uint64_t m = (uint64_t)rng_u32(st) * (uint64_t)n;
+        if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+    }
+}
+/* SliceRandom::shuffle (rand 0.8 seq/mod.rs): i from len-1 down to 1, swap i with gen_index(i + 1). */
+static void shuffle256(int *a, uint64_t *st) {
+    for (int i = 0; i < 256; i++) a[i] = i;
+    for (uint32_t i = 255; i >= 1; i--) {
+        uint32_t j = rng_below(st, i + 1);
+        int t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+    }
+}
+/* Perlin::new (noise.rs:23-42) on the k-th NoiseTexture's stream. */
+static void perlin_new(uint64_t seed, uint32_t k, perlin_t *P) {
+    uint64_t st = or_mix64(seed ^ 0x50455246494E4F49ull) + (uint64_t)(k + 1) * 0xD1B54A32D192ED03ull;
+    shuffle256(P->perm_x, &st);
+    shuffle256(P->perm_y, &st);
+    shuffle256(P->perm_z, &st);
+    for (int i = 0; i < 256; i++) (void)or_gen_f64(&st); /* ranfloat: drawn, never read */
+    double s11 = or_uniform_incl_scale(-1.0, 1.0);
+    for (int i = 0; i < 256; i++) { /* Vector3d::random(-1, 1): x, y, z draws (algebra/mod.rs:59-66) */
+        double x = uniform_sample(&st, -1.0, s11);
+        double y = uniform_sample(&st, -1.0, s11);
+        double z = uniform_sample(&st, -1.0, s11);
+        P->ranvec[i] = V(x, y, z);
+    }
+}
+/* `f64 as i32`: saturating, NaN -> 0 */
+static int32_t as_i32(double x) {
+    if (isnan(x)) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+static uint32_t as_u32(double x) {
+    if (isnan(x) || x <= 0.0) return 0;
+    if (x >= 4294967295.0) return UINT32_MAX;
+    return (uint32_t)x;
+}
+/* Perlin::noise (noise.rs:44-74): cartesian = (0..3).map(|_| 0..2).multi_cartesian_product()
+ * (last coordinate fastest); (d + x) & 255 with wrapping i32 add; terms summed in order. */
+static double perlin_noise(const perlin_t *P, v3 p) {
+    int32_t x = as_i32(floor(p.x)), y = as_i32(floor(p.y)), z = as_i32(floor(p.z));
+    double u = p.x - floor(p.x), v = p.y - floor(p.y), w = p.z - floor(p.z);
+    double u2 = u * u * (3.0 - 2.0 * u);
+    double v2 = v * v * (3.0 - 2.0 * v);
+    double w2 = w * w * (3.0 - 2.0 * w);
+    double sum = 0.0;
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++)
+            for (int c = 0; c < 2; c++) {
+                int ix = (int)(((uint32_t)a + (uint32_t)x) & 255u);
+                int iy = (int)(((uint32_t)b + (uint32_t)y) & 255u);
+                int iz = (int)(((uint32_t)c + (uint32_t)z) & 255u);
+                v3 g = P->ranvec[P->perm_x[ix] ^ P->perm_y[iy] ^ P->perm_z[iz]];
+                double fi = (double)a, fj = (double)b, fk = (double)c;
+                double term = (fi * u2 + (double)(1 - a) * (1.0 - u2)) * (fj * v2 + (double)(1 - b) * (1.0 - v2)) *
+                              (fk * w2 + (double)(1 - c) * (1.0 - w2)) * vdot(g, V(u - fi, v - fj, w - fk));
+                sum = sum + term;
+            }
+    return sum;
+}
+/* Perlin::turb (noise.rs:76-88): the scan multiplies weight into noise(p) of
+ * the ORIGINAL p every octave (temp_p is updated but never read). */
+static double perlin_turb(const perlin_t *P, v3 p, int depth) {
+    double weight = 1.0, sum = 0.0;
+    for (int i = 0; i < depth; i++) {
+        double ret = weight * perlin_noise(P, p);
+        weight *= 0.5;
+        sum = sum + ret;
+    }
+    return fabs(sum);
+}
+void or_perlin_tables(uint64_t seed, uint32_t k, int32_t perm[768], double ranvec[768]) {
+    perlin_t P;
+    perlin_new(seed, k, &P);
+    for (int i = 0; i < 256; i++) {
+        perm[i] = P.perm_x[i];
+        perm[256 + i] = P.perm_y[i];
+        perm[512 + i] = P.perm_z[i];
+        vstore(ranvec + 3 * i, P.ranvec[i]);
+    }
+}
+double or_perlin_turb(uint64_t seed, uint32_t k, const double p[3]) {
+    perlin_t P;
+    perlin_new(seed, k, &P);
+    return perlin_turb(&P, vload(p), 7);
+}
+static v3 texture_value(const or_scene *sc, int node, double u, double v, v3 p) {
+    const or_texture_in *t = &sc->tex[node];
+    switch (t->type) {
+    case OR_TEX_SOLID: return vload(t->c); /* :15-20 */
+    case OR_TEX_CHECKER: { /* :40-51 */
+        double sines = sin(t->c[0] * p.x) * sin(t->c[1] * p.y) * sin(t->c[2] * p.z);
+        return texture_value(sc, sines < 0.0 ? t->odd : t->even, u, v, p);
+    }
+    case OR_TEX_UVCHECKER: { /* :76-87 */
+        double sines = sin(v * t->c[0] * M_PI) * sin(u * t->c[1] * M_PI);
+        return texture_value(sc, sines < 0.0 ? t->odd : t->even, u, v, p);
+    }
+    case OR_TEX_NOISE: { /* :60-66 */
+        double a = 0.5 * (1.0 + sin(t->c[0] * p.z + 10.0 * perlin_turb(&sc->perlin[node], p, 7)));
+        return V(1.0 * a, 1.0 * a, 1.0 * a);
+    }
+    case OR_TEX_IMAGE: { /* :96-116; get_pixel would panic at x == width / y == height: clamped */
+        const image_t *im = &sc->images[t->aux];
+        double uc = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);
+        double vc = 1.0 - (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
+        uint32_t x = as_u32(uc * (double)im->w), y = as_u32(vc * (double)im->h);
+        if (x >= im->w) x = im->w - 1;
+        if (y >= im->h) y = im->h - 1;
+        const uint8_t *q = im->rgba + ((size_t)y * im->w + x) * 4;
+        double cs = 1.0 / 255.0;
+        return V((double)q[0] * cs, (double)q[1] * cs, (double)q[2] * cs);
+    }
+    }
+    return V(NAN, NAN, NAN);
+}
+void or_scene_set_textures(or_scene *s, const or_texture_in *tex, int ntex, uint64_t seed) {
+    free(s->tex);
+    free(s->perlin);
+    s->tex = malloc(sizeof(or_texture_in) * (ntex > 0 ? ntex : 1));
+    s->perlin = calloc(ntex > 0 ? ntex : 1, sizeof(perlin_t));
+    s->ntex = ntex;
+    uint32_t k = 0;
+    for (int i = 0; i < ntex; i++) {
+        s->tex[i] = tex[i];
+        if (tex[i].type == OR_TEX_NOISE) perlin_new(seed, k++, &s->perlin[i]);
+    }
+}
+int or_scene_add_image(or_scene *s, uint32_t width, uint32_t height, const uint8_t *rgba) {
+    s->images = realloc(s->images, sizeof(image_t) * (s->nimages + 1));
+    image_t *im = &s->images[s->nimages];
+    im->w = width;
+    im->h = height;
+    im->rgba = malloc((size_t)width * height * 4);
+    memcpy(im->rgba, rgba, (size_t)width * height * 4);
+    return s->nimages++;
+}
+void or_texture_value(const or_scene *s, int tex, double u, double v, const double p[3], double out[3]) {
+    vstore(out, texture_value(s, tex, u, v, vload(p)));
+}
+
+/* ======================================================================= */
 /* Materials (src/world/material.rs)                                       */
 /* ======================================================================= */
 static v3 random_in_unit_sphere(uint64_t *rng, double s11, or_stats *st) { /* algebra/mod.rs:77-84 */
@@ -955,8 +1173,8 @@ static v3 random_in_unit_sphere(uint64_t *rng, double s11, or_stats *st) { /* al
     }
 }
 /* returns 1 if scattered (ray + attenuation), 0 if absorbed */
-static int scatter(const mat_t *m, v3 rd, const or_hit *h, uint64_t *rng, double s11, v3 *no, v3 *nd,
-                   v3 *att, or_stats *st) {
+static int scatter(const or_scene *sc, const mat_t *m, v3 rd, const or_hit *h, uint64_t *rng, double s11, v3 *no,
+                   v3 *nd, v3 *att, or_stats *st) {
     v3 n = vload(h->normal), p = vload(h->point);
     if (st && m->type >= 0 && m->type < 5) st->scatters[m->type]++;
     switch (m->type) {
@@ -965,7 +1183,7 @@ static int scatter(const mat_t *m, v3 rd, const or_hit *h, uint64_t *rng, double
         if (vis_zero(dir)) dir = n;
         *no = p;
         *nd = vnorm(dir);
-        *att = m->albedo;
+        *att = m->tex < 0 ? m->albedo : texture_value(sc, m->tex, h->u, h->v, p);
         return 1;
     }
     case OR_METAL: { /* material.rs:63-76 */
@@ -973,7 +1191,7 @@ static int scatter(const mat_t *m, v3 rd, const or_hit *h, uint64_t *rng, double
         v3 dir = m->fuzz == 0.0 ? refl : vadd(refl, vscale(random_in_unit_sphere(rng, s11, st), m->fuzz));
         *no = p;
         *nd = vnorm(dir);
-        *att = m->albedo;
+        *att = m->tex < 0 ? m->albedo : texture_value(sc, m->tex, h->u, h->v, p);
         return 1;
     }
     case OR_DIELECTRIC: { /* material.rs:92-115, reflectance :84-88 */
@@ -998,8 +1216,9 @@ static int scatter(const mat_t *m, v3 rd, const or_hit *h, uint64_t *rng, double
     default: return 0; /* DiffuseLight / EmptyMaterial: Material::scatter default None */
     }
 }
-static v3 emitted(const mat_t *m) { /* material.rs:124-128, 22-31 */
-    return m->type == OR_DIFFUSE_LIGHT ? m->emit : V(0.0, 0.0, 0.0);
+static v3 emitted(const or_scene *sc, const mat_t *m, const or_hit *h) { /* material.rs:124-128, 22-31 */
+    if (m->type != OR_DIFFUSE_LIGHT) return V(0.0, 0.0, 0.0);
+    return m->tex < 0 ? m->emit : texture_value(sc, m->tex, h->u, h->v, vload(h->point));
 }
 /* Scene::background: src/world/mod.rs:199-202 (ignores the JSON value) */
 static v3 background(v3 d) {
@@ -1017,9 +1236,9 @@ static v3 ray_color_rec(const or_scene *sc, v3 o, v3 d, uint32_t depth, uint64_t
     if (depth == 0) return V(0.0, 0.0, 0.0);
     const mat_t *m = &sc->mats[h.material];
     v3 no, nd, att;
-    if (scatter(m, d, &h, rng, s11, &no, &nd, &att, st))
+    if (scatter(sc, m, d, &h, rng, s11, &no, &nd, &att, st))
         return vprod(att, ray_color_rec(sc, no, nd, depth - 1, rng, s11, st));
-    return emitted(m);
+    return emitted(sc, m, &h);
 }
 void or_ray_color(const or_scene *sc, const double o[3], const double d[3], uint32_t depth,
                   uint64_t *rng_state, double out[3], or_stats *st) {

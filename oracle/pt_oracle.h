@@ -59,13 +59,27 @@ typedef struct {
     double fa, fb, fc, fd, fr; /* ray-marched function: a, b, c, d, sphere_radius */
 } or_shape_in;
 
+/* textures (src/world/texture.rs) */
+#define OR_TEX_SOLID 0
+#define OR_TEX_CHECKER 1
+#define OR_TEX_UVCHECKER 2
+#define OR_TEX_NOISE 3
+#define OR_TEX_IMAGE 4
+
 typedef struct {
-    int32_t type, pad0;
+    int32_t type;
+    int32_t tex; /* -1: SolidColor in albedo / emit; else the root texture node */
     double albedo[3];
     double fuzz;
     double ior;
     double emit[3];
 } or_material_in;
+
+/* texture tree node: checker kinds pick child odd/even; image: aux = image index */
+typedef struct {
+    int32_t type, odd, even, aux;
+    double c[3]; /* colour | CheckerTexture multipliers | UVChecker multipliers | noise scale */
+} or_texture_in;
 
 typedef struct {
     int32_t type, material, inverse_normal, depth, func, pad0;
@@ -79,6 +93,7 @@ typedef struct {
     double point[3];
     double normal[3];
     int32_t front_face, shape, material, pad0;
+    double u, v; /* RayHit u, v (texture coordinates) */
 } or_hit;
 
 typedef struct {
@@ -108,6 +123,16 @@ typedef struct {
 or_scene *or_scene_new(const or_shape_in *shapes, int n, const or_material_in *mats, int nm,
                        int random_spheres, uint64_t scene_seed);
 void or_scene_free(or_scene *s);
+/* Non-solid textures: the node array (pre-order per material, as the JSON
+ * lists them) and the images they reference (RGBA8, row-major).  The k-th
+ * NoiseTexture node draws its Perlin tables from stream k of seed. */
+void or_scene_set_textures(or_scene *s, const or_texture_in *tex, int ntex, uint64_t seed);
+int or_scene_add_image(or_scene *s, uint32_t width, uint32_t height, const uint8_t *rgba);
+/* Perlin::new tables of stream k (perm: 3 x 256, ranvec: 256 x 3) and Perlin::turb(p, 7). */
+void or_perlin_tables(uint64_t seed, uint32_t k, int32_t perm[768], double ranvec[768]);
+double or_perlin_turb(uint64_t seed, uint32_t k, const double p[3]);
+/* Texture::value of node `tex` at (u, v, p). */
+void or_texture_value(const or_scene *s, int tex, double u, double v, const double p[3], double out[3]);
 int or_scene_num_shapes(const or_scene *s);
 int or_scene_num_materials(const or_scene *s);
 void or_scene_get_shape(const or_scene *s, int i, or_shape_out *out);

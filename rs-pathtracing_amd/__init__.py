@@ -53,8 +53,14 @@ class PtError(RuntimeError):
         self.code = code
 
 
+# pt_image_loader: (user, filename, *width, *height, *rgba8) -> status
+ImageLoader = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                          C.POINTER(C.POINTER(C.c_uint8)))
+
+
 class SceneOpts(C.Structure):
-    _fields_ = [("random_spheres", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_uint64)]
+    _fields_ = [("random_spheres", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_uint64),
+                ("load_image", ImageLoader), ("image_user", C.c_void_p)]
 
 
 class CameraStruct(C.Structure):
@@ -72,7 +78,7 @@ class ShapeInfo(C.Structure):
 
 
 class MaterialInfo(C.Structure):
-    _fields_ = [("type", C.c_int32), ("pad0", C.c_int32), ("albedo", C.c_double * 3),
+    _fields_ = [("type", C.c_int32), ("texture", C.c_int32), ("albedo", C.c_double * 3),
                 ("fuzz", C.c_double), ("ior", C.c_double), ("emit", C.c_double * 3)]
 
 
@@ -201,9 +207,29 @@ class Scene:
         self._h = handle
 
     @classmethod
-    def from_json(cls, data: str | bytes, random_spheres: bool = True, seed: int = 1) -> "Scene":
+    def from_json(cls, data: str | bytes, random_spheres: bool = True, seed: int = 1,
+                  images: dict | None = None) -> "Scene":
+        """images: ImageTexture file name -> (width, height, RGBA8 bytes), the
+        decoded pixels the reference gets from image::open(..).into_rgba8()
+        (src/world/texture.rs:119-130).  Names not in it are read by the
+        library's built-in binary-PPM reader."""
         raw = data.encode("utf-8") if isinstance(data, str) else bytes(data)
         opts = SceneOpts(1 if random_spheres else 0, 0, seed)
+        keep = []
+        if images:
+            def load(_user, name, w, h, px):
+                img = images.get(name.decode("utf-8"))
+                if img is None:
+                    return PT_ERR_UNSUPPORTED  # declined: the built-in PPM reader takes it
+                iw, ih, rgba = img
+                if len(rgba) != iw * ih * 4:
+                    return PT_ERR_INVALID
+                buf = (C.c_uint8 * len(rgba)).from_buffer_copy(rgba)
+                keep.append(buf)
+                w[0], h[0] = iw, ih
+                px[0] = C.cast(buf, C.POINTER(C.c_uint8))
+                return PT_OK
+            opts.load_image = ImageLoader(load)
         h = C.c_void_p()
         _check(lib().pt_scene_create_from_json(raw, len(raw), C.byref(opts), C.byref(h)))
         return cls(h)
@@ -296,7 +322,8 @@ class HipRenderer(Renderer):
 
     def render_device(self, camera: Camera, width: int, height: int, spp: int, seed: int, rank: int,
                       world: int, out_ptr: int, stream_ptr: int = 0):
-        """Render this rank's tiles into device memory at out_ptr (see pt_render_device)."""
+        """Render this rank's tiles into device memory at out_ptr on the HIP stream stream_ptr
+        (0 = the null stream; see pt_render_device)."""
         _check(lib().pt_render_device(self._h, C.byref(camera._c), width, height, spp, seed, rank, world,
                                       C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
 

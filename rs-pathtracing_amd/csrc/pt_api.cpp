@@ -90,10 +90,15 @@ int pt_scene_create_from_json(const char *json, size_t len, const pt_scene_opts 
     *out = nullptr;
     bool rs = opts ? opts->random_spheres != 0 : true;
     uint64_t seed = opts ? opts->seed : 1;
+    ImageSource img;
+    if (opts) {
+        img.load = opts->load_image;
+        img.user = opts->image_user;
+    }
     try {
         pt_scene *s = new pt_scene;
         try {
-            s->s = scene_from_json(json, len, rs, seed);
+            s->s = scene_from_json(json, len, rs, seed, img);
         } catch (...) {
             delete s;
             throw;
@@ -149,6 +154,7 @@ int pt_scene_get_material(const pt_scene *s, int i, pt_material_info *o) {
     const HostMaterial &m = s->s.materials[i];
     std::memset(o, 0, sizeof *o);
     o->type = m.type;
+    o->texture = m.tex;
     for (int k = 0; k < 3; k++) {
         o->albedo[k] = m.albedo[k];
         o->emit[k] = m.emit[k];
@@ -203,6 +209,13 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     upload(&r->ds.lin, acc.lin);
     upload(&r->ds.march, acc.march);
     upload(&r->ds.boxes, acc.boxes);
+    const Scene &S = scene->s;
+    if (!S.textures.empty()) {
+        upload(&r->ds.tex, S.textures);
+        upload(&r->ds.perlin, S.perlins);
+        upload(&r->ds.images, S.images);
+        upload(&r->ds.pixels, S.pixels);
+    }
     if (err != hipSuccess) {
         pt_renderer_destroy(r);
         return hip_fail(err, "uploading the scene");
@@ -237,6 +250,10 @@ void pt_renderer_destroy(pt_renderer *r) {
     if (r->ds.lin) (void)hipFree(r->ds.lin);
     if (r->ds.march) (void)hipFree(r->ds.march);
     if (r->ds.boxes) (void)hipFree(r->ds.boxes);
+    if (r->ds.tex) (void)hipFree(r->ds.tex);
+    if (r->ds.perlin) (void)hipFree(r->ds.perlin);
+    if (r->ds.images) (void)hipFree(r->ds.images);
+    if (r->ds.pixels) (void)hipFree(r->ds.pixels);
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     wave_workspace_free(&r->ws);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -356,7 +373,9 @@ int pt_render_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t 
     P.compact = world > 1 ? 1 : 0;
     P.tile_begin = 0;
     P.tile_count = pt_shard_tiles(w, h, rank, world);
-    hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+    // any HIP stream, 0 being the null stream as everywhere in HIP (pt_unshard_device
+    // takes the same handle, so a caller's render -> gather -> unshard stays ordered)
+    hipStream_t st = (hipStream_t)stream;
     HIP_TRY(launch_render(r->ds, P, d_out, st, &r->ws));
     return PT_OK;
 }

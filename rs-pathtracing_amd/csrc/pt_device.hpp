@@ -250,6 +250,10 @@ struct Scene {
     const int32_t *__restrict__ lin;
     const int32_t *__restrict__ march;
     const DBox *__restrict__ boxes;
+    const DTexture *__restrict__ tex;  // non-solid texture trees (null when the scene has none)
+    const DPerlin *__restrict__ perlin;
+    const DImage *__restrict__ images;
+    const uint8_t *__restrict__ pixels;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
 };
 
@@ -369,6 +373,127 @@ PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
     return h;
 }
 
+// (u, v) of a hit as each ray_intersect computes them from the object-space
+// point (only textures read them): Sphere shapes/mod.rs:361-373, Rectangle
+// :189-190, Cube :263-282, ray-marched shapes ray_marching.rs:60 (Heart, Sine,
+// Star :170, :239, :302 give (0, 0); DupinCyclide, HuntsSurface, Cushion
+// :371, :436, :506 give (p.x, p.y)).
+PT_HD void hit_uv(const DShape &s, const Ray &r, double t, double *u, double *v) {
+    V3 o = xf_point(s.inv, r.o);
+    V3 d = xf_vector(s.inv, r.d);
+    V3 p = v3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+    const double PI = 3.141592653589793;
+    switch (s.type) {
+    case SPHERE: {
+        const double theta = acos(-p.y);
+        const double phi = atan2(-p.z, p.x) + PI;
+        *u = phi / (2.0 * PI);
+        *v = theta / PI;
+        return;
+    }
+    case RECTANGLE:
+        *u = (p.x - s.p[0]) / (s.p[2] - s.p[0]);
+        *v = (p.y - s.p[1]) / (s.p[3] - s.p[1]);
+        return;
+    case CUBE: {
+        double ax = fabs(p.x), ay = fabs(p.y), az = fabs(p.z);
+        double mc = fmax(fmax(ax, ay), az);
+        if (mc == ax) *u = p.y, *v = p.z;
+        else if (mc == ay) *u = p.x, *v = p.z;
+        else if (mc == az) *u = p.x, *v = p.y;
+        else *u = *v = __builtin_nan("");
+        return;
+    }
+    default:
+        if (s.func == march::F_DUPIN || s.func == march::F_HUNTS || s.func == march::F_CUSHION) *u = p.x, *v = p.y;
+        else *u = *v = 0.0;
+        return;
+    }
+}
+
+// Rust `f64 as i32` / `as u32`: saturating, NaN -> 0.
+PT_HD int32_t sat_i32(double x) {
+    if (!(x == x)) return 0;
+    if (x >= 2147483647.0) return 2147483647;
+    if (x <= -2147483648.0) return -2147483647 - 1;
+    return (int32_t)x;
+}
+PT_HD uint32_t sat_u32(double x) {
+    if (!(x > 0.0)) return 0u;
+    if (x >= 4294967295.0) return 4294967295u;
+    return (uint32_t)x;
+}
+
+// Perlin::noise (src/algebra/noise.rs:44-74): the 8 corners in
+// multi_cartesian_product order (last index fastest), summed in order.
+PT_HD double perlin_noise(const DPerlin &P, V3 p) {
+    const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    const uint32_t x = (uint32_t)sat_i32(fx), y = (uint32_t)sat_i32(fy), z = (uint32_t)sat_i32(fz);
+    const double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const double u2 = u * u * (3.0 - 2.0 * u);
+    const double v2 = v * v * (3.0 - 2.0 * v);
+    const double w2 = w * w * (3.0 - 2.0 * w);
+    double acc = 0.0;
+    for (int c = 0; c < 8; c++) {
+        const int d0 = c >> 2, d1 = (c >> 1) & 1, d2 = c & 1;
+        const int32_t k = P.perm[0][(x + (uint32_t)d0) & 255u] ^ P.perm[1][(y + (uint32_t)d1) & 255u] ^
+                          P.perm[2][(z + (uint32_t)d2) & 255u];
+        const double fi = (double)d0, fj = (double)d1, fk = (double)d2;
+        const double dot = P.ranvec[k][0] * (u - fi) + P.ranvec[k][1] * (v - fj) + P.ranvec[k][2] * (w - fk);
+        acc = acc + (fi * u2 + (double)(1 - d0) * (1.0 - u2)) * (fj * v2 + (double)(1 - d1) * (1.0 - v2)) *
+                        (fk * w2 + (double)(1 - d2) * (1.0 - w2)) * dot;
+    }
+    return acc;
+}
+// Perlin::turb (:76-88) as the reference runs it: every octave samples the
+// unscaled p (its temp_p is never read), weights 1, 1/2, ..., 1/64.
+PT_HD double perlin_turb(const DPerlin &P, V3 p) {
+    const double n = perlin_noise(P, p);
+    double acc = 0.0, weight = 1.0;
+    for (int i = 0; i < 7; i++) {
+        acc = acc + weight * n;
+        weight *= 0.5;
+    }
+    return fabs(acc);
+}
+
+// Texture::value (src/world/texture.rs) down the tree from `node`.
+PT_HD V3 tex_value(const Scene &sc, int node, double u, double v, V3 p) {
+    const double PI = 3.141592653589793;
+    for (int guard = 0; guard < 64; guard++) {
+        const DTexture &t = sc.tex[node];
+        switch (t.type) {
+        case TEX_SOLID: return v3(t.c[0], t.c[1], t.c[2]);
+        case TEX_CHECKER: {  // :40-51
+            const double sines = sin(t.c[0] * p.x) * sin(t.c[1] * p.y) * sin(t.c[2] * p.z);
+            node = sines < 0.0 ? t.odd : t.even;
+            break;
+        }
+        case TEX_UVCHECKER: {  // :76-87
+            const double sines = sin(v * t.c[0] * PI) * sin(u * t.c[1] * PI);
+            node = sines < 0.0 ? t.odd : t.even;
+            break;
+        }
+        case TEX_NOISE: {  // :60-66
+            const double s = 0.5 * (1.0 + sin(t.c[0] * p.z + 10.0 * perlin_turb(sc.perlin[t.aux], p)));
+            return v3(1.0 * s, 1.0 * s, 1.0 * s);
+        }
+        default: {  // TEX_IMAGE :96-116 (get_pixel panics at u = 1 or v = 0; clamped here)
+            const DImage im = sc.images[t.aux];
+            const double uc = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);
+            const double vc = 1.0 - (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
+            uint32_t x = sat_u32(uc * (double)im.width), y = sat_u32(vc * (double)im.height);
+            x = x < im.width ? x : im.width - 1;
+            y = y < im.height ? y : im.height - 1;
+            const uint8_t *px = sc.pixels + im.offset + ((size_t)y * im.width + x) * 4;
+            const double cs = 1.0 / 255.0;
+            return v3((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+        }
+        }
+    }
+    return v3(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
+}
+
 // Diagnostic phase timing (TIMING build only): wave-level s_memtime deltas.
 struct PhaseTimes {
     uint64_t trace, march, select, shade, passes, march_passes, finish, scatter, restart;
@@ -412,10 +537,24 @@ PT_HD V3 background(V3 d) {
 // on the way back up its recursion (renderer/mod.rs:29-33).  Only albedo
 // attenuations are pushed (Dielectric's (1,1,1) is an exact identity), as
 // 32-bit material ids in NW 64-bit words, unwound after the leaf radiance.
+// A textured albedo depends on the hit: its value is stored at the entry's
+// level in memory (vb[(level * 3 + c) * vs]) and the entry is VAL_BIT.
+constexpr uint32_t VAL_BIT = 0x80000000u;
 template <int NW>
 struct IdStack {
     uint64_t w[NW];
     int n;
+    double *vb = nullptr;  // textured attenuation values (scenes with textures only)
+    size_t vs = 0;
+    PT_HD void push_val(V3 a) {
+        vb[(size_t)(n * 3 + 0) * vs] = a.x;
+        vb[(size_t)(n * 3 + 1) * vs] = a.y;
+        vb[(size_t)(n * 3 + 2) * vs] = a.z;
+        push(VAL_BIT);
+    }
+    PT_HD V3 val(int level) const {
+        return v3(vb[(size_t)(level * 3 + 0) * vs], vb[(size_t)(level * 3 + 1) * vs], vb[(size_t)(level * 3 + 2) * vs]);
+    }
     PT_HD void clear() {
 #pragma unroll
         for (int i = 0; i < NW; i++) w[i] = 0;
@@ -442,7 +581,9 @@ struct IdStack {
 // Everything in a bounce after the closest hit (who, t) is known.
 // Stack: any type with push(id), pop() and a count n (IdStack in registers,
 // or the wavefront engine's per-slot id array in HBM).
-template <bool STATS = false, int FK = march::F_ANY, class Stack>
+// TEX: the build for scenes with non-solid textures (textured albedos are
+// evaluated at the hit and pushed by value; textured lights emit their value).
+template <bool STATS = false, int FK = march::F_ANY, bool TEX = false, class Stack>
 PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, Stack &stk, Rng &rng,
                  double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
@@ -458,18 +599,26 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     Hit h = finish<FK>(s, ray, t);
     const DMaterial &m = sc.mats[s.material];
     if (tfin) *tfin = PT_STAMP();
+    // the texture value at this hit (RayHit u, v and world point)
+    auto textured = [&]() {
+        double u, v;
+        hit_uv(s, ray, t, &u, &v);
+        return tex_value(sc, m.tex, u, v, h.p);
+    };
     V3 dir;
     if (m.type == LAMBERTIAN) {  // material.rs:41-54
         if (STATS) ct->c[C_LAMBERT]++;
         V3 u = normalize(random_in_unit_sphere<STATS>(rng, s11, ct));
         dir = add(h.n, u);
         if (approx_zero(dir.x) && approx_zero(dir.y) && approx_zero(dir.z)) dir = h.n;
-        stk.push((uint32_t)s.material);
+        if (TEX && m.tex >= 0) stk.push_val(textured());
+        else stk.push((uint32_t)s.material);
     } else if (m.type == METAL) {  // :63-76
         if (STATS) ct->c[C_METAL]++;
         V3 rf = reflect(ray.d, h.n);
         dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
-        stk.push((uint32_t)s.material);
+        if (TEX && m.tex >= 0) stk.push_val(textured());
+        else stk.push((uint32_t)s.material);
     } else if (m.type == DIELECTRIC) {  // :92-115
         if (STATS) ct->c[C_DIELECTRIC]++;
         double ratio = h.front ? 1.0 / m.ior : m.ior;
@@ -485,7 +634,8 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         }
         dir = refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio);
     } else {  // DiffuseLight / EmptyMaterial: no scatter, emitted()
-        *leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
+        if (TEX && m.type == DIFFUSE_LIGHT && m.tex >= 0) *leaf = textured();
+        else *leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
         return true;
     }
     ray.o = h.p;
@@ -494,34 +644,44 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     return false;
 }
 
-template <int NW, bool STATS = false>
+template <int NW, bool STATS = false, bool TEX = false>
 PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng, double s11, V3 *leaf,
                   Ctr *ct = nullptr) {
     double t;
     if (STATS) ct->c[C_BOUNCES]++;
     int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
-    return shade<STATS>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
+    return shade<STATS, march::F_ANY, TEX>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
 }
 
-template <bool STATS = false, class Stack>
+template <bool STATS = false, bool TEX = false, class Stack>
 PT_HD V3 unwind(const Scene &sc, Stack &stk, V3 c, Ctr *ct = nullptr) {
     while (stk.n > 0) {
         if (STATS) ct->c[C_UNWIND]++;
-        const DMaterial &m = sc.mats[stk.pop()];
-        c = v3(m.albedo[0] * c.x, m.albedo[1] * c.y, m.albedo[2] * c.z);  // Vector3d::product
+        const uint32_t id = stk.pop();
+        if (TEX && (id & VAL_BIT)) {
+            const V3 a = stk.val(stk.n);
+            c = v3(a.x * c.x, a.y * c.y, a.z * c.z);
+        } else {
+            const DMaterial &m = sc.mats[id];
+            c = v3(m.albedo[0] * c.x, m.albedo[1] * c.y, m.albedo[2] * c.z);  // Vector3d::product
+        }
     }
     return c;
 }
 
 // ray_color (src/renderer/mod.rs:23-45), iterative with the recursion's product order.
-template <int NW>
-PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s11) {
+// vb, vs: the textured-attenuation area of this lane (TEX builds).
+template <int NW, bool TEX = false>
+PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s11, double *vb = nullptr,
+                   size_t vs = 0) {
     IdStack<NW> stk;
     stk.clear();
+    stk.vb = vb;
+    stk.vs = vs;
     V3 leaf;
-    while (!bounce<NW>(sc, ray, depth, stk, rng, s11, &leaf)) {
+    while (!bounce<NW, false, TEX>(sc, ray, depth, stk, rng, s11, &leaf)) {
     }
-    return unwind(sc, stk, leaf);
+    return unwind<false, TEX>(sc, stk, leaf);
 }
 
 // Camera sample: MultisamplerRayCaster::next (ray_caster.rs:103-118), u then v.
@@ -554,9 +714,9 @@ constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
 enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
 
 
-template <int NW, bool STATS = false, bool TIMING = false, int FK = march::F_ANY>
+template <int NW, bool STATS = false, bool TIMING = false, int FK = march::F_ANY, bool TEX = false>
 PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr,
-                     PhaseTimes *pt = nullptr) {
+                     PhaseTimes *pt = nullptr, double *vb = nullptr, size_t vs = 0) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
     V3 acc = v3(0.0, 0.0, 0.0);
     uint32_t s = 0;
@@ -565,6 +725,8 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
     uint32_t depth = P.depth;
     IdStack<NW> stk;
     stk.clear();
+    stk.vb = vb;
+    stk.vs = vs;
     const int nmarch = (sc.diag & 1) ? 0 : sc.nmarch;
     int phase = PH_TRACE, who = -1, km = 0, mshape = -1;
     double best = 0.0;
@@ -636,8 +798,8 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_SHADE) {
             V3 leaf;
             uint64_t tf = 0;
-            const bool ended = shade<STATS, FK>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
-                                                TIMING ? &tf : nullptr);
+            const bool ended = shade<STATS, FK, TEX>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
+                                                     TIMING ? &tf : nullptr);
             if (TIMING) {
                 uint64_t n = PT_STAMP();
                 if (tf) {
@@ -647,7 +809,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                 ts = n;
             }
             if (ended) {
-                acc = add(acc, unwind<STATS>(sc, stk, leaf, ct));
+                acc = add(acc, unwind<STATS, TEX>(sc, stk, leaf, ct));
                 if (STATS) ct->c[C_SAMPLES]++;
                 if (++s == P.spp) break;
                 rng.s = sample_key(P.seed, pixel, s);

@@ -84,16 +84,18 @@ __global__ __launch_bounds__(256) void closest_hit_probe(dev::Scene sc, const do
     out[i] = h;
 }
 
+// Probes of textured scenes keep textured attenuation values in `vals`:
+// lane i, level k, component c at vals[(k * 3 + c) * n + i].
 template <int NW>
 __global__ __launch_bounds__(256) void ray_color_probe(dev::Scene sc, const double *__restrict__ rays, uint64_t *__restrict__ states,
-                                size_t n, uint32_t depth, double s11, double *__restrict__ out) {
+                                size_t n, uint32_t depth, double s11, double *__restrict__ out, double *vals) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ray r;
     r.o = dev::v3(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
     r.d = dev::v3(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
     dev::Rng rng{states[i]};
-    V3 c = dev::ray_color<NW>(sc, r, depth, rng, s11);
+    V3 c = vals ? dev::ray_color<NW, true>(sc, r, depth, rng, s11, vals + i, n) : dev::ray_color<NW>(sc, r, depth, rng, s11);
     states[i] = rng.s;
     out[i * 3 + 0] = c.x;
     out[i * 3 + 1] = c.y;
@@ -102,11 +104,13 @@ __global__ __launch_bounds__(256) void ray_color_probe(dev::Scene sc, const doub
 
 template <int NW>
 __global__ __launch_bounds__(256) void trace_pixels_probe(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
-                                   double *__restrict__ out) {
+                                   double *__restrict__ out, double *vals) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t idx = pixels[i];
-    V3 c = dev::trace_pixel<NW>(sc, P, idx % P.width, idx / P.width);
+    V3 c = vals ? dev::trace_pixel<NW, false, false, march::F_ANY, true>(sc, P, idx % P.width, idx / P.width, nullptr,
+                                                                         nullptr, vals + i, n)
+                : dev::trace_pixel<NW>(sc, P, idx % P.width, idx / P.width);
     out[i * 3 + 0] = c.x;
     out[i * 3 + 1] = c.y;
     out[i * 3 + 2] = c.z;
@@ -116,13 +120,17 @@ __global__ __launch_bounds__(256) void trace_pixels_probe(dev::Scene sc, FramePa
 // with one 64-bit atomic per counter per lane.  Only pt_count_work uses it.
 template <int NW>
 __global__ __launch_bounds__(256) void count_work(dev::Scene sc, FrameParams P, const uint32_t *__restrict__ pixels, size_t n,
-                           unsigned long long *__restrict__ ctr) {
+                           unsigned long long *__restrict__ ctr, double *vals) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ctr c;
     for (int k = 0; k < C_COUNT; k++) c.c[k] = 0;
     uint32_t idx = pixels[i];
-    dev::trace_pixel<NW, true>(sc, P, idx % P.width, idx / P.width, &c);
+    if (vals)
+        dev::trace_pixel<NW, true, false, march::F_ANY, true>(sc, P, idx % P.width, idx / P.width, &c, nullptr,
+                                                              vals + i, n);
+    else
+        dev::trace_pixel<NW, true>(sc, P, idx % P.width, idx / P.width, &c);
     for (int k = 0; k < C_COUNT; k++)
         if (c.c[k]) atomicAdd(&ctr[k], (unsigned long long)c.c[k]);
 }
@@ -200,6 +208,10 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.lin = s.lin;
     d.march = s.march;
     d.boxes = s.boxes;
+    d.tex = s.tex;
+    d.perlin = s.perlin;
+    d.images = s.images;
+    d.pixels = s.pixels;
     d.nnodes = s.nnodes;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
@@ -245,6 +257,7 @@ hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double
                               WaveWorkspace *ws, int fkind);
 
 static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
+    if (s.tex) return true;  // textured scenes: the megakernel keeps attenuation ids in registers only
     const char *e = getenv("PT_ENGINE");
     if (e && e[0] == 'm') return false;
     if (e && e[0] == 'w') return ws != nullptr;
@@ -293,27 +306,50 @@ hipError_t launch_closest_hit(const DeviceScene &s, const double *rays, size_t n
     return hipGetLastError();
 }
 
+// Stream-ordered scratch for the probes' textured attenuation values (textured
+// scenes only): n lanes x (depth + 1) levels x 3 doubles.
+struct ProbeVals {
+    double *p = nullptr;
+    hipStream_t st;
+    hipError_t alloc(const DeviceScene &s, size_t n, uint32_t depth) {
+        if (!s.tex) return hipSuccess;
+        return hipMallocAsync((void **)&p, n * (depth + 1) * 3 * sizeof(double), st);
+    }
+    ~ProbeVals() {
+        if (p) (void)hipFreeAsync(p, st);
+    }
+};
+
 hipError_t launch_ray_color(const DeviceScene &s, const double *rays, uint64_t *states, size_t n, uint32_t depth,
                             double s11, double *out, hipStream_t st) {
     if (!n) return hipSuccess;
+    ProbeVals vals{nullptr, st};
+    hipError_t e = vals.alloc(s, n, depth);
+    if (e != hipSuccess) return e;
     PT_DISPATCH_NW(depth, (ray_color_probe<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-                              dscene(s), rays, states, n, depth, s11, out)));
+                              dscene(s), rays, states, n, depth, s11, out, vals.p)));
     return hipGetLastError();
 }
 
 hipError_t launch_trace_pixels(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
                                double *out, hipStream_t st) {
     if (!n) return hipSuccess;
+    ProbeVals vals{nullptr, st};
+    hipError_t e = vals.alloc(s, n, P.depth);
+    if (e != hipSuccess) return e;
     PT_DISPATCH_NW(P.depth, (trace_pixels_probe<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-                                dscene(s), P, pixels, n, out)));
+                                dscene(s), P, pixels, n, out, vals.p)));
     return hipGetLastError();
 }
 
 hipError_t launch_count_work(const DeviceScene &s, const FrameParams &P, const uint32_t *pixels, size_t n,
                              unsigned long long *ctr, hipStream_t st) {
     if (!n) return hipSuccess;
+    ProbeVals vals{nullptr, st};
+    hipError_t e = vals.alloc(s, n, P.depth);
+    if (e != hipSuccess) return e;
     PT_DISPATCH_NW(P.depth, (count_work<NW><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(dscene(s), P, pixels, n,
-                                                                                         ctr)));
+                                                                                         ctr, vals.p)));
     return hipGetLastError();
 }
 
@@ -327,6 +363,7 @@ hipError_t launch_march_probe(const double *jobs, size_t n, double *t, int32_t *
 hipError_t launch_render_timed(const DeviceScene &s, const FrameParams &P, double *out, unsigned long long *acc,
                                hipStream_t st) {
     if (P.tile_count == 0) return hipSuccess;
+    if (s.tex) return hipErrorNotSupported;  // the timing build has no textured attenuation store
     render_tiles_timed<<<P.tile_count, 256, 0, st>>>(dscene(s), P, out, acc);
     return hipGetLastError();
 }

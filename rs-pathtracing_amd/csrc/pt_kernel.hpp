@@ -13,6 +13,10 @@ struct DeviceScene {
     DNode *nodes = nullptr;
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
+    DTexture *tex = nullptr;  // non-solid textures (null when the scene has none)
+    DPerlin *perlin = nullptr;
+    DImage *images = nullptr;
+    uint8_t *pixels = nullptr;
     int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
     int fkind = 0;  // 0: every marched shape is a Heart (or none) -> Heart-only kernel builds; -1: any
 };

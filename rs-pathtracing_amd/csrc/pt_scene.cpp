@@ -6,6 +6,9 @@
 #include "pt_scene.hpp"
 
 #include <cmath>
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 
@@ -43,6 +46,17 @@ struct Stream {  // SplitMix64 (the thread_rng stand-in), rand 0.8 conversions
         double v;
         std::memcpy(&v, &bits, 8);
         return (v - 1.0) * scale + lo;
+    }
+    // Rng::gen::<u32>: the high half of the next 64-bit output (RNG spec)
+    uint32_t next_u32() { return (uint32_t)(next() >> 32); }
+    // gen_range(0..n) for u32 (rand 0.8.5 UniformInt::sample_single_inclusive
+    // over [0, n-1]): widening multiply, rejection above the shifted zone
+    uint32_t below(uint32_t n) {
+        const uint32_t zone = (n << __builtin_clz(n)) - 1u;
+        for (;;) {
+            const uint64_t m = (uint64_t)next_u32() * n;
+            if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+        }
     }
 };
 
@@ -225,6 +239,7 @@ DMaterial to_device(const HostMaterial &m) {
     DMaterial d;
     std::memset(&d, 0, sizeof d);
     d.type = m.type;
+    d.tex = m.tex;
     for (int k = 0; k < 3; k++) {
         d.albedo[k] = m.albedo[k];
         d.emit[k] = m.emit[k];
@@ -297,33 +312,140 @@ void transform(const Value &v, HostShape &s) {
     if (!hs) schema("missing field `scale`");
     transform_new(t, r, sc, s.direct, s.inverse);
 }
-// Texture (src/world/texture.rs): only SolidColor (:10-20) on the GPU path.
-void solid_color(const Value &tex, double out[3]) {
-    std::string t = str(field(tex, "type"), "type");
-    if (t == "SolidColor") {
-        vec3(field(tex, "color"), out, "color");
-        return;
+// Binary PPM (P6, maxval 255) -> RGBA8: the built-in ImageTexture reader.
+bool read_ppm(const std::string &path, uint32_t *w, uint32_t *h, std::vector<uint8_t> *rgba) {
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    auto token = [&](std::string *out) {
+        out->clear();
+        int c = std::fgetc(f);
+        for (;;) {  // whitespace and # comments
+            while (c != EOF && std::isspace(c)) c = std::fgetc(f);
+            if (c != '#') break;
+            while (c != EOF && c != '\n') c = std::fgetc(f);
+        }
+        while (c != EOF && !std::isspace(c)) {
+            out->push_back((char)c);
+            c = std::fgetc(f);
+        }
+        return !out->empty();
+    };
+    std::string m, sw, sh, sv;
+    bool ok = token(&m) && m == "P6" && token(&sw) && token(&sh) && token(&sv) && sv == "255";
+    long W = ok ? std::atol(sw.c_str()) : 0, H = ok ? std::atol(sh.c_str()) : 0;
+    ok = ok && W > 0 && H > 0 && W < (1l << 16) && H < (1l << 16);
+    std::vector<uint8_t> rgb;
+    if (ok) {
+        rgb.resize((size_t)W * H * 3);
+        ok = std::fread(rgb.data(), 1, rgb.size(), f) == rgb.size();
     }
-    if (t == "CheckerTexture" || t == "NoiseTexture" || t == "UVChecker" || t == "ImageTexture")
-        unsupported("texture `" + t + "` is not implemented on the GPU path");
-    schema("unknown variant `" + t + "` of Texture");
+    std::fclose(f);
+    if (!ok) return false;
+    *w = (uint32_t)W;
+    *h = (uint32_t)H;
+    rgba->resize((size_t)W * H * 4);
+    for (size_t i = 0; i < (size_t)W * H; i++) {  // into_rgba8: opaque alpha
+        (*rgba)[i * 4 + 0] = rgb[i * 3 + 0];
+        (*rgba)[i * 4 + 1] = rgb[i * 3 + 1];
+        (*rgba)[i * 4 + 2] = rgb[i * 3 + 2];
+        (*rgba)[i * 4 + 3] = 255;
+    }
+    return true;
 }
-HostMaterial material(const Value &m) {
+
+// Texture (src/world/texture.rs), typetag "type".  Non-solid textures become
+// nodes of sc.textures in pre-order (a node, then its odd subtree, then its
+// even one); the k-th NoiseTexture in that order draws its Perlin tables from
+// stream k of the scene seed.
+struct TexCtx {
+    Scene *sc;
+    uint64_t seed;
+    const ImageSource *img;
+};
+int32_t texture_node(const Value &tex, TexCtx &cx) {
+    std::string t = str(field(tex, "type"), "type");
+    Scene &sc = *cx.sc;
+    const int32_t id = (int32_t)sc.textures.size();
+    sc.textures.push_back(DTexture{});
+    DTexture d{};
+    d.odd = d.even = d.aux = -1;
+    if (t == "SolidColor") {  // :10-20
+        d.type = TEX_SOLID;
+        vec3(field(tex, "color"), d.c, "color");
+    } else if (t == "CheckerTexture") {  // :22-51 (the JSON `scale` key is not a field: ignored)
+        d.type = TEX_CHECKER;
+        vec3(field(tex, "multipliers"), d.c, "multipliers");
+        d.odd = texture_node(field(tex, "odd"), cx);
+        d.even = texture_node(field(tex, "even"), cx);
+    } else if (t == "UVChecker") {  // :68-87, multipliers: (f64, f64)
+        d.type = TEX_UVCHECKER;
+        const Value &m = field(tex, "multipliers");
+        if (m.kind != Value::Array || m.arr.size() != 2) schema("invalid type, expected a tuple of size 2 for `multipliers`");
+        d.c[0] = num(m.arr[0], "multipliers");
+        d.c[1] = num(m.arr[1], "multipliers");
+        d.odd = texture_node(field(tex, "odd"), cx);
+        d.even = texture_node(field(tex, "even"), cx);
+    } else if (t == "NoiseTexture") {  // :53-66, noise skipped by serde -> Perlin::new()
+        d.type = TEX_NOISE;
+        d.c[0] = num(field(tex, "scale"), "scale");
+        d.aux = (int32_t)sc.perlins.size();
+        sc.perlins.push_back(DPerlin{});
+        perlin_new(cx.seed, (uint32_t)d.aux, &sc.perlins.back());
+    } else if (t == "ImageTexture") {  // :89-131, image::open(image_filename).into_rgba8()
+        d.type = TEX_IMAGE;
+        const std::string fn = str(field(tex, "image_filename"), "image_filename");
+        uint32_t w = 0, h = 0;
+        std::vector<uint8_t> own;
+        const uint8_t *px = nullptr;
+        int rc = PT_ERR_UNSUPPORTED;
+        if (cx.img->load) {
+            rc = cx.img->load(cx.img->user, fn.c_str(), &w, &h, &px);
+            if (rc != PT_ERR_UNSUPPORTED && (rc != PT_OK || !px || !w || !h))
+                throw SceneError{PT_ERR_INVALID, "Could not open texture file: " + fn};
+        }
+        if (rc == PT_ERR_UNSUPPORTED) {  // no loader, or it declined: the built-in reader
+            if (!read_ppm(fn, &w, &h, &own))
+                throw SceneError{PT_ERR_UNSUPPORTED, "Could not open texture file: " + fn +
+                                                         " (without an image loader only binary PPM is read)"};
+            px = own.data();
+        }
+        DImage im;
+        im.offset = sc.pixels.size();
+        im.width = w;
+        im.height = h;
+        sc.pixels.insert(sc.pixels.end(), px, px + (size_t)w * h * 4);
+        d.aux = (int32_t)sc.images.size();
+        sc.images.push_back(im);
+    } else {
+        schema("unknown variant `" + t + "` of Texture");
+    }
+    sc.textures[id] = d;
+    return id;
+}
+// A material's albedo / emit: SolidColor inline (tex = -1), else a tree.
+int32_t texture(const Value &tex, TexCtx &cx, double solid[3]) {
+    if (str(field(tex, "type"), "type") == "SolidColor") {
+        vec3(field(tex, "color"), solid, "color");
+        return -1;
+    }
+    return texture_node(tex, cx);
+}
+HostMaterial material(const Value &m, TexCtx &cx) {
     HostMaterial h;
     std::string t = str(field(m, "type"), "type");
     if (t == "Lambertian") {  // material.rs:35-54
         h.type = LAMBERTIAN;
-        solid_color(field(m, "albedo"), h.albedo);
+        h.tex = texture(field(m, "albedo"), cx, h.albedo);
     } else if (t == "Metal") {  // :56-76
         h.type = METAL;
-        solid_color(field(m, "albedo"), h.albedo);
+        h.tex = texture(field(m, "albedo"), cx, h.albedo);
         h.fuzz = num(field(m, "fuzz"), "fuzz");
     } else if (t == "Dielectric") {  // :78-116
         h.type = DIELECTRIC;
         h.ior = num(field(m, "index_of_refraction"), "index_of_refraction");
     } else if (t == "DiffuseLight") {  // :118-128
         h.type = DIFFUSE_LIGHT;
-        solid_color(field(m, "emit"), h.emit);
+        h.tex = texture(field(m, "emit"), cx, h.emit);
     } else if (t == "EmptyMaterial") {  // :130-134
         h.type = EMPTY;
     } else {
@@ -331,6 +453,31 @@ HostMaterial material(const Value &m) {
     }
     return h;
 }
+
+}  // namespace
+
+// Perlin::new (src/algebra/noise.rs:23-42) on the k-th NoiseTexture's stream:
+// shuffle perm_x, perm_y, perm_z (SliceRandom::shuffle: for i = 255..1, swap
+// i with gen_range(0..i+1)), draw the 256 unused ranfloat values, then ranvec
+// = 256 x Vector3d::random(-1, 1) (algebra/mod.rs:59-66, not normalised).
+void perlin_new(uint64_t seed, uint32_t k, DPerlin *out) {
+    Stream rng{mix64(seed ^ 0x50455246494E4F49ull) + (uint64_t)(k + 1) * 0xD1B54A32D192ED03ull};
+    for (int a = 0; a < 3; a++) {
+        for (int i = 0; i < 256; i++) out->perm[a][i] = i;
+        for (uint32_t i = 255; i >= 1; i--) {
+            const uint32_t j = rng.below(i + 1);
+            const int32_t t = out->perm[a][i];
+            out->perm[a][i] = out->perm[a][j];
+            out->perm[a][j] = t;
+        }
+    }
+    for (int i = 0; i < 256; i++) (void)rng.gen();  // ranfloat
+    const double s11 = uniform_incl_scale(-1.0, 1.0);
+    for (int i = 0; i < 256; i++)
+        for (int c = 0; c < 3; c++) out->ranvec[i][c] = rng.uniform(-1.0, s11);
+}
+
+namespace {
 
 // add_random_spheres (src/world/json_models.rs:50-133) with a seeded stream.
 void add_random_spheres(Scene &sc, uint64_t seed) {
@@ -372,7 +519,7 @@ void add_random_spheres(Scene &sc, uint64_t seed) {
 
 }  // namespace
 
-Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_t seed) {
+Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_t seed, const ImageSource &images) {
     Value root;
     try {
         root = ptjson::parse(json, len);
@@ -398,9 +545,10 @@ Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_
     const Value &mats = field(root, "materials");
     if (mats.kind != Value::Object) schema("invalid type, expected a map for `materials`");
     std::unordered_map<std::string, int32_t> index;
+    TexCtx cx{&sc, seed, &images};
     for (auto &kv : mats.obj) {
         index[kv.first] = (int32_t)sc.materials.size();  // a repeated key keeps the last value
-        sc.materials.push_back(material(kv.second));
+        sc.materials.push_back(material(kv.second, cx));
     }
 
     // shapes: Vec<Box<dyn ShapeJson>> (typetag "type"), file order

@@ -23,6 +23,7 @@ struct HostShape {
 
 struct HostMaterial {
     int32_t type = EMPTY;
+    int32_t tex = -1;  // root texture node, -1: SolidColor (albedo / emit hold the colour)
     double albedo[3] = {0, 0, 0};
     double fuzz = 0, ior = 0;
     double emit[3] = {0, 0, 0};
@@ -34,6 +35,18 @@ struct Scene {
     pt_camera camera;
     int json_shapes = 0;  // shapes from the JSON file; random spheres follow
     double background[3];  // parsed but unused, as in the reference (src/world/mod.rs:199-202)
+    // non-solid textures: tree nodes, one Perlin table per NoiseTexture, images
+    std::vector<DTexture> textures;
+    std::vector<DPerlin> perlins;
+    std::vector<DImage> images;
+    std::vector<uint8_t> pixels;
+};
+
+// ImageTexture decoding (image::open, src/world/texture.rs:119-130) is the
+// host's: the C-ABI caller may pass a loader; binary PPM (P6) is built in.
+struct ImageSource {
+    pt_image_loader load = nullptr;
+    void *user = nullptr;
 };
 
 // Throws SceneError on bad input (converted to a status code at the C-ABI).
@@ -42,7 +55,10 @@ struct SceneError {
     std::string msg;
 };
 
-Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_t seed);
+Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_t seed,
+                      const ImageSource &images = ImageSource());
+// Perlin::new (src/algebra/noise.rs:23-42) from the k-th NoiseTexture's stream of the scene seed.
+void perlin_new(uint64_t seed, uint32_t k, DPerlin *out);
 
 void transform_new(const double t[3], const double r[3], const double s[3], double direct[4][4],
                    double inverse[4][4]);

@@ -22,11 +22,32 @@ struct alignas(64) DShape {
 };
 static_assert(sizeof(DShape) == 320, "DShape is five cache lines");
 
+// tex: -1 when the albedo (Lambertian, Metal) or emit (DiffuseLight) texture
+// is a SolidColor, whose colour is stored here; otherwise the root DTexture.
 struct alignas(8) DMaterial {
-    int32_t type, pad;
+    int32_t type, tex;
     double albedo[3];
     double fuzz, ior;
     double emit[3];
+};
+
+// Texture tree node (src/world/texture.rs).  Checker nodes choose their odd or
+// even child node; SolidColor, NoiseTexture and ImageTexture are leaves.
+enum TextureKind : int32_t { TEX_SOLID = 0, TEX_CHECKER = 1, TEX_UVCHECKER = 2, TEX_NOISE = 3, TEX_IMAGE = 4 };
+struct alignas(8) DTexture {
+    int32_t type, odd, even, aux;  // aux: Perlin table (noise) or image index
+    double c[3];  // SolidColor color | CheckerTexture multipliers | UVChecker multipliers (2) | noise scale
+};
+// Perlin (src/algebra/noise.rs:6-42): the three permutations and ranvec
+// (ranfloat is drawn but never read by the texture).
+struct DPerlin {
+    int32_t perm[3][256];
+    double ranvec[256][3];
+};
+// ImageTexture pixels (RGBA8, row-major) in the scene's pixel pool.
+struct DImage {
+    uint64_t offset;
+    uint32_t width, height;
 };
 
 // Threaded (skip-pointer) BVH node over shapes, DFS order: on an AABB hit go

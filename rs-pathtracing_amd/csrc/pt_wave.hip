@@ -50,6 +50,7 @@ struct WfView {
     int32_t *who;    // best hit shape (-1: miss)
     uint32_t *meta;  // depth | stack count << 8
     uint32_t *ids;   // attenuation-id stack: entry k of a path at ids[k * cap + id]
+    double *att;     // textured attenuation values (TEX builds): (k * 3 + c) * cap + id
     double *rx, *ry, *rz;  // sample radiance of finished paths
     uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
     uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
@@ -72,6 +73,17 @@ struct MemStack {
     uint32_t *base;
     size_t stride;
     int n;
+    double *vb;  // textured attenuation values: level k, component c at vb[(k * 3 + c) * stride]
+    __device__ __forceinline__ void push_val(V3 a) {
+        vb[(size_t)(n * 3 + 0) * stride] = a.x;
+        vb[(size_t)(n * 3 + 1) * stride] = a.y;
+        vb[(size_t)(n * 3 + 2) * stride] = a.z;
+        push(dev::VAL_BIT);
+    }
+    __device__ __forceinline__ V3 val(int level) const {
+        return dev::v3(vb[(size_t)(level * 3 + 0) * stride], vb[(size_t)(level * 3 + 1) * stride],
+                       vb[(size_t)(level * 3 + 2) * stride]);
+    }
     __device__ __forceinline__ void push(uint32_t id) {
         base[(size_t)n * stride] = id;
         n++;
@@ -105,7 +117,7 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
 // DIAG: wave-level s_memtime cycles per section (load + shade, trace,
 // march pre-check, stores) summed into diag[36..39] (tuning only).
-template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY>
+template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool TEX = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -126,7 +138,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         Ray ray;
         dev::Rng rng{0};
         uint32_t depth = 0;
-        MemStack stk{v.ids, (size_t)v.cap, 0};
+        MemStack stk{v.ids, (size_t)v.cap, 0, nullptr};
         if (live) {
             if (FIRST) {
                 id = i;
@@ -148,9 +160,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
+                if (TEX) stk.vb = v.att + id;
                 V3 leaf;
-                if (dev::shade<false, FK>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
-                    const V3 c = dev::unwind(sc, stk, leaf);
+                if (dev::shade<false, FK, TEX>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                    const V3 c = dev::unwind<false, TEX>(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
                     v.rz[id] = c.z;
@@ -610,6 +623,10 @@ static int bounce_waves() {
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
                           const WfView &v, int it, unsigned long long *diag, int fkind) {
+    if (sc.tex) {  // non-solid textures: the generic textured build
+        wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        return;
+    }
     if (fkind != march::F_HEART) {  // another ray-marched function: the generic build
         wf_bounce<NW, FIRST, 2, false, march::F_ANY><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
@@ -695,8 +712,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     hipError_t e = ensure_streams(ws, slots);
     if (e != hipSuccess) return e;
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+    const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
     const size_t slot_bytes = al((size_t)cap * 8) * 11 + al((size_t)cap * 4) * 4 + al((size_t)cap * 4 * (P0.depth + 1)) +
-                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 8) + al(cnt_words * 4);
+                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 8) + al(cnt_words * 4) +
+                              al(att_bytes);
     const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
     e = reserve(ws, bytes);
     if (e != hipSuccess) return e;
@@ -729,6 +748,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
         sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
         v.cnt = (uint32_t *)take(cnt_words * 4);
+        v.att = att_bytes ? (double *)take(att_bytes) : nullptr;
         v.cap = cap;
     }
     double *acc = (double *)take((size_t)npix_max * 24);

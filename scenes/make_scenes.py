@@ -9,6 +9,8 @@ arrangement.  The schema is SceneJson (src/world/json_models.rs:23-29).
     python scenes/make_scenes.py            # writes cornell_box.json, spheres.json
     python scenes/make_scenes.py --synthetic N   # also synthetic_N.json (config C5)
 
+textured.json and noise.json exercise every texture (CheckerTexture,
+UVChecker, NoiseTexture, ImageTexture on textures/grid.ppm; texture.rs).
 marched.json exercises every ray-marched ShapeFunction of the reference
 (Heart, Sine, Star, DupinCyclide, HuntsSurface, Cushion;
 src/world/shapes/ray_marching.rs:121-520) on a ground plane under a light.
@@ -127,6 +129,86 @@ def marched():
     }
 
 
+def checker(odd, even, mult=(5, 5, 5)):
+    return {"type": "CheckerTexture", "scale": 4.0, "odd": solid(odd), "even": solid(even),
+            "multipliers": {"x": mult[0], "y": mult[1], "z": mult[2]}}
+
+
+def uvchecker(odd, even, mult=(40, 40)):
+    return {"type": "UVChecker", "scale": 4.0, "odd": solid(odd), "even": solid(even), "multipliers": list(mult)}
+
+
+def textured():
+    """Every texture of src/world/texture.rs on every shape kind that carries
+    u, v: the detached_materials.json arrangement (checker Metal ground, UV-
+    checker spheres, an image-mapped Metal sphere, a Cushion) plus a noise
+    sphere, a textured cube and rectangle, and a checker-textured light."""
+    shapes = [
+        {"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+         "material": "Ground"},
+        {"type": "Sphere", "name": "Ball", "transform": tr((-2.2, 1, 0), (0, 30, 0)), "material": "UV"},
+        {"type": "Sphere", "name": "Earth", "transform": tr((0, 1, 0), (0, 0, 0)), "material": "EarthMap"},
+        {"type": "Sphere", "name": "Marble", "transform": tr((2.2, 1, 0)), "material": "Marble"},
+        {"type": "Cube", "name": "Box", "transform": tr((-1.1, 0.45, -2.2), (0, 25, 0), (0.45, 0.45, 0.45)),
+         "material": "UV"},
+        {"type": "Rectangle", "x0": -1, "x1": 1, "y0": 0, "y1": 1.5, "transform": tr((0, 0, 2.5), (0, 180, 0)),
+         "material": "Poster"},
+        {"type": "Rectangle", "x0": -2, "x1": 2, "y0": -1, "y1": 1, "transform": tr((0, 5, 0), (90, 0, 0)),
+         "material": "Sun"},
+        {"type": "BruteForsableShape", "name": "Cushion", "shape": {"type": "Cushion", "sphere_radius": 1.5},
+         "step": 0.01, "depth": 3, "transform": tr((1.2, 0.5, -2.4), (-70, 20, 0), (0.45, 0.45, 0.45)),
+         "material": "UV"},
+    ]
+    return {
+        "camera": {"position": [0, 2.2, -9], "direction": [0, -0.2, 1], "up": [0, 1, 0], "fov": 40,
+                   "focal_length": 1},
+        "shapes": shapes,
+        "materials": {
+            "Ground": {"type": "Metal", "albedo": checker((0.1, 0.2, 0.8), (0.9, 0.2, 0.1)), "fuzz": 0.0},
+            "UV": {"type": "Lambertian", "albedo": uvchecker((0.1, 0.9, 0.9), (0.9, 0.1, 0.9))},
+            "EarthMap": {"type": "Metal", "albedo": {"type": "ImageTexture",
+                                                     "image_filename": "./scenes/textures/grid.ppm"}, "fuzz": 1},
+            "Poster": {"type": "Lambertian", "albedo": {"type": "ImageTexture",
+                                                        "image_filename": "./scenes/textures/grid.ppm"}},
+            "Marble": {"type": "Lambertian", "albedo": {"type": "NoiseTexture", "scale": 4.0}},
+            "Sun": {"type": "DiffuseLight", "emit": checker((4, 4, 4), (9, 8, 7), (3, 3, 3))},
+        },
+        "background": [0, 0, 0],
+    }
+
+
+def noise():
+    """light_source.json's arrangement: NoiseTexture ground and sphere under a
+    rectangle light (no ray-marched shape)."""
+    return {
+        "camera": {"position": [13, 2, 3], "direction": [-13, -1, -3], "up": [0, 1, 0], "fov": 30,
+                   "focal_length": 1},
+        "shapes": [
+            {"type": "Rectangle", "x0": -1, "x1": 1, "y0": -1, "y1": 1, "transform": tr((0, 5, -2), (45, 0, 0)),
+             "material": "Light"},
+            {"type": "Sphere", "name": "Sphere1", "transform": tr((0, 2, 0), s=(2, 2, 2)), "material": "Ground"},
+            {"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+             "material": "Ground"},
+        ],
+        "materials": {
+            "Ground": {"type": "Lambertian", "albedo": {"type": "NoiseTexture", "scale": 4.0}},
+            "Light": {"type": "DiffuseLight", "emit": solid((4, 4, 4))},
+        },
+        "background": [0, 0, 0],
+    }
+
+
+def grid_ppm(w=64, h=32):
+    """A small RGB test image (binary PPM): a colour ramp with a grid, so that
+    every texel of an image-mapped sphere is distinguishable."""
+    px = bytearray()
+    for y in range(h):
+        for x in range(w):
+            line = x % 8 == 0 or y % 8 == 0
+            px += bytes((255, 255, 255) if line else ((x * 4) % 256, (y * 8) % 256, (x * y) % 256))
+    return b"P6\n%d %d\n255\n" % (w, h) + bytes(px)
+
+
 def synthetic(n, seed=1):
     """C5: n small spheres on a jittered grid (add_random_spheres recipe scaled up,
     json_models.rs:73-133), a Lambertian ground sphere and the spheres.json camera."""
@@ -169,6 +251,10 @@ def main():
     (HERE / "cornell_box.json").write_text(json.dumps(cornell(), indent=1) + "\n")
     (HERE / "spheres.json").write_text(json.dumps(spheres(), indent=1) + "\n")
     (HERE / "marched.json").write_text(json.dumps(marched(), indent=1) + "\n")
+    (HERE / "textured.json").write_text(json.dumps(textured(), indent=1) + "\n")
+    (HERE / "noise.json").write_text(json.dumps(noise(), indent=1) + "\n")
+    (HERE / "textures").mkdir(exist_ok=True)
+    (HERE / "textures" / "grid.ppm").write_bytes(grid_ppm())
     if a.synthetic:
         (HERE / ("synthetic_%d.json" % a.synthetic)).write_text(json.dumps(synthetic(a.synthetic)) + "\n")
 

@@ -35,6 +35,11 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.lin = b->acc.lin.data();
         b->view.march = b->acc.march.data();
         b->view.boxes = b->acc.boxes.data();
+        const bool tex = !b->sc.textures.empty();
+        b->view.tex = tex ? b->sc.textures.data() : nullptr;
+        b->view.perlin = tex ? b->sc.perlins.data() : nullptr;
+        b->view.images = tex ? b->sc.images.data() : nullptr;
+        b->view.pixels = tex ? b->sc.pixels.data() : nullptr;
         b->view.nnodes = (int)b->acc.nodes.size();
         b->view.nlin = (int)b->acc.lin.size();
         b->view.nmarch = (int)b->acc.march.size();
@@ -76,8 +81,9 @@ extern "C" void h_ray_color(void *p, const double *ray, uint64_t *state, uint32_
     r.o = dev::v3(ray[0], ray[1], ray[2]);
     r.d = dev::v3(ray[3], ray[4], ray[5]);
     dev::Rng rng{*state};
-    dev::V3 c = depth <= 8 ? dev::ray_color<4>(b->view, r, depth, rng, b->s11)
-                           : dev::ray_color<32>(b->view, r, depth, rng, b->s11);
+    std::vector<double> vals((depth + 1) * 3);  // textured attenuation values of this one lane
+    dev::V3 c = depth <= 8 ? dev::ray_color<4, true>(b->view, r, depth, rng, b->s11, vals.data(), 1)
+                           : dev::ray_color<32, true>(b->view, r, depth, rng, b->s11, vals.data(), 1);
     *state = rng.s;
     out[0] = c.x, out[1] = c.y, out[2] = c.z;
 }
@@ -94,9 +100,12 @@ extern "C" void h_trace_pixels(void *p, uint32_t w, uint32_t h, uint32_t spp, ui
     P.height = h;
     P.spp = spp;
     P.depth = depth;
+    std::vector<double> vals((depth + 1) * 3);
     for (size_t i = 0; i < n; i++) {
-        dev::V3 c = depth <= 8 ? dev::trace_pixel<4>(b->view, P, pixels[i] % w, pixels[i] / w)
-                               : dev::trace_pixel<32>(b->view, P, pixels[i] % w, pixels[i] / w);
+        dev::V3 c = depth <= 8 ? dev::trace_pixel<4, false, false, march::F_ANY, true>(
+                                     b->view, P, pixels[i] % w, pixels[i] / w, nullptr, nullptr, vals.data(), 1)
+                               : dev::trace_pixel<32, false, false, march::F_ANY, true>(
+                                     b->view, P, pixels[i] % w, pixels[i] / w, nullptr, nullptr, vals.data(), 1);
         out[3 * i] = c.x, out[3 * i + 1] = c.y, out[3 * i + 2] = c.z;
     }
 }
@@ -117,9 +126,14 @@ extern "C" void h_count_work(void *p, uint32_t w, uint32_t h, uint32_t spp, uint
     P.depth = depth;
     Ctr c;
     std::memset(&c, 0, sizeof c);
+    std::vector<double> vals((depth + 1) * 3);
     for (size_t i = 0; i < n; i++) {
-        if (depth <= 8) dev::trace_pixel<4, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c);
-        else dev::trace_pixel<32, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c);
+        if (depth <= 8)
+            dev::trace_pixel<4, true, false, march::F_ANY, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c, nullptr,
+                                                                 vals.data(), 1);
+        else
+            dev::trace_pixel<32, true, false, march::F_ANY, true>(b->view, P, pixels[i] % w, pixels[i] / w, &c,
+                                                                  nullptr, vals.data(), 1);
     }
     for (int k = 0; k < C_COUNT; k++) counters[k] = c.c[k];
 }

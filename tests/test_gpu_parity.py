@@ -370,3 +370,70 @@ def test_kernel_timing_from_first_frame(pt, cornell):
     assert kt["bounce"][1] > 0 and kt["bounce"][0] > 0.0
     assert kt["march"][1] > 0 and kt["select"][1] > 0 and kt["reduce"][1] > 0
     assert np.array_equal(img, r.render(cam, ip, 2, seed=4))
+
+
+# ---------------------------------------------------------------- textures
+# The texture lookups call sin / acos / atan2, which the GPU evaluates with
+# the ROCm device math library and the oracle with glibc (as the reference
+# does through Rust's std).  Both are faithful to within an ulp but not always
+# equal: a NoiseTexture value (a sin) can differ in its last bit (measured:
+# <= 2.2e-15 relative, 1-4 % of pixels), and a checker or texel boundary could
+# flip for a rare sample.  The bar: the north_star RMS tolerance, and all but a
+# rare pixel within 1e-12 relative of the oracle.
+TEX_REL = 1e-12
+TEX_CLOSE_MIN = 0.998
+
+
+@pytest.mark.parametrize("name,seed,depth", [("textured.json", 1, 8), ("noise.json", 2, 8),
+                                             ("textured.json", 3, 50)])
+def test_textured_frames(pt, name, seed, depth, monkeypatch):
+    from conftest import ROOT, scene_text
+    monkeypatch.chdir(ROOT)
+    text = scene_text(name)
+    scenes = (pt.Scene.from_json(text, seed=seed), O.Scene(text, seed=seed))
+    img, ref = render_pair(pt, scenes, 64, 36, 4, depth, seed=seed)
+    check_image_tol(img, ref)
+    assert img.mean() > 0.05
+
+
+def check_image_tol(img, ref):
+    assert np.all(np.isfinite(img))
+    assert np.all(rms(img, ref) <= RMS_TOL), rms(img, ref)
+    close = np.mean(np.all(np.abs(img - ref) <= TEX_REL * np.abs(ref), axis=1))
+    assert close >= TEX_CLOSE_MIN, "pixels within %g relative: %.6f" % (TEX_REL, close)
+
+
+def test_textured_probes_and_shards(pt, monkeypatch):
+    from conftest import ROOT, scene_text
+    monkeypatch.chdir(ROOT)
+    text = scene_text("textured.json")
+    ps, osc = pt.Scene.from_json(text, seed=4), O.Scene(text, seed=4)
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h = 96, 54
+    rng = np.random.default_rng(8)
+    pixels = rng.choice(w * h, size=300, replace=False).astype(np.uint32)
+    got = r.trace_pixel_samples(cam, pt.ImageParams(w, h), 3, pixels, seed=6)
+    ref = osc.render(w, h, 3, 8, 6, pixels=pixels)
+    check_image_tol(got, ref)
+    rays = random_rays(500, rng, [-3, 0.1, -4], [3, 3, 3], eye=[0, 2.2, -9])
+    states = rng.integers(0, 2 ** 63, size=len(rays), dtype=np.uint64)
+    st_gpu = states.copy()
+    col = r.ray_color(rays, st_gpu, depth=8)
+    refc = np.array([osc.ray_color(ray[:3], ray[3:], 8, int(s))[0] for ray, s in zip(rays, states)])
+    check_image_tol(col, refc)
+    # tile shards of a textured frame reassemble to the single-GPU frame
+    full = r.render(cam, pt.ImageParams(w, h), 2, seed=1)
+    world = 3
+    per = pt.shard_tiles(w, h, 0, world)
+    import torch
+    stream = torch.cuda.current_stream().cuda_stream  # order after torch's zero-fills
+    shards = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda")
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    for k in range(world):
+        r.render_device(cam, w, h, 2, 1, k, world, shards.data_ptr() + k * per * 256 * 3 * 8, stream)
+    pt.unshard_device(shards.data_ptr(), w, h, world, frame.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.view(-1, 3).cpu().numpy(), full)
+    cnt = pt.count_work(r, cam, pt.ImageParams(w, h), 2, pixels, seed=1)
+    assert cnt["samples"] == 2 * len(pixels)

@@ -89,8 +89,11 @@ def test_errors(pt):
     js["shapes"][0].update(radius=1, tube_radius=0.2)
     expect(pt, js, pt.PT_ERR_UNSUPPORTED)
     js = base_scene()
-    js["materials"]["M"]["albedo"] = {"type": "NoiseTexture", "scale": 4}
-    expect(pt, js, pt.PT_ERR_UNSUPPORTED)
+    js["materials"]["M"]["albedo"] = {"type": "NoiseTexture"}  # `scale` is required
+    assert "scale" in expect(pt, js, pt.PT_ERR_PARSE)
+    js = base_scene()
+    js["materials"]["M"]["albedo"] = {"type": "ImageTexture", "image_filename": "/nonexistent/earthmap.jpg"}
+    assert "earthmap.jpg" in expect(pt, js, pt.PT_ERR_UNSUPPORTED)  # no loader: PPM only
     js = base_scene()
     js["shapes"][0]["type"] = "Banana"
     expect(pt, js, pt.PT_ERR_PARSE)

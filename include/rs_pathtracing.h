@@ -36,6 +36,7 @@ extern "C" {
 #define PT_RECTANGLE 1 /* src/world/shapes/mod.rs:150-221 */
 #define PT_CUBE 2      /* src/world/shapes/mod.rs:223-302 */
 #define PT_MARCH 3     /* RayMarchingShape, src/world/shapes/ray_marching.rs:10-110 */
+#define PT_TORUS 4     /* src/world/shapes/mod.rs:400-494 */
 #define PT_FUNC_HEART 0 /* ShapeFunctions, ray_marching.rs:121-520 */
 #define PT_FUNC_SINE 1
 #define PT_FUNC_STAR 2
@@ -85,6 +86,7 @@ typedef struct {
     double direct[16], inverse[16];
     double x0, y0, x1, y1, step;
     double a, b, c, d, sphere_radius; /* ray-marched function parameters (JSON) */
+    double radius, tube_radius;       /* Torus */
 } pt_shape_info;
 
 typedef struct {
@@ -173,7 +175,7 @@ int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *camera, uint32_t wid
  * attempts, march jumps, hits, Lambertian/Metal/Dielectric scatters,
  * rejection-sampling tries, attenuation multiplies.  Used for the FLOP side
  * of the roofline. */
-#define PT_NUM_COUNTERS 17
+#define PT_NUM_COUNTERS 18
 int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
                   uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
                   uint64_t *counters);

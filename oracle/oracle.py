@@ -21,7 +21,7 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "liboracle.so"
 
-SPHERE, RECT, CUBE, MARCH = 0, 1, 2, 3
+SPHERE, RECT, CUBE, MARCH, TORUS = 0, 1, 2, 3, 4
 FUNC_HEART, FUNC_SINE, FUNC_STAR, FUNC_DUPIN, FUNC_HUNTS, FUNC_CUSHION = 0, 1, 2, 3, 4, 5
 FUNC_IDS = {"Heart": FUNC_HEART, "Sine": FUNC_SINE, "Star": FUNC_STAR, "DupinCyclide": FUNC_DUPIN,
             "HuntsSurface": FUNC_HUNTS, "Cushion": FUNC_CUSHION}
@@ -34,7 +34,7 @@ class ShapeIn(C.Structure):
                 ("translate", C.c_double * 3), ("rotate", C.c_double * 3), ("scale", C.c_double * 3),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
                 ("step", C.c_double), ("fa", C.c_double), ("fb", C.c_double), ("fc", C.c_double),
-                ("fd", C.c_double), ("fr", C.c_double)]
+                ("fd", C.c_double), ("fr", C.c_double), ("radius", C.c_double), ("tube_radius", C.c_double)]
 
 
 class MaterialIn(C.Structure):
@@ -56,7 +56,7 @@ class ShapeOut(C.Structure):
                 ("direct", C.c_double * 16), ("inverse", C.c_double * 16),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
                 ("step", C.c_double), ("fa", C.c_double), ("fb", C.c_double), ("fc", C.c_double),
-                ("fd", C.c_double), ("fr", C.c_double)]
+                ("fd", C.c_double), ("fr", C.c_double), ("radius", C.c_double), ("tube_radius", C.c_double)]
 
 
 class Hit(C.Structure):
@@ -114,6 +114,7 @@ def lib():
     L.or_perlin_tables.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_int32), d3]
     L.or_perlin_turb.restype = C.c_double
     L.or_perlin_turb.argtypes = [C.c_uint64, C.c_uint32, d3]
+    L.or_solve_quartic.argtypes = [C.c_double] * 5 + [d3, d3]
     L.or_texture_value.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_double, d3, d3]
     L.or_scene_num_shapes.argtypes = [C.c_void_p]
     L.or_scene_num_materials.argtypes = [C.c_void_p]
@@ -284,6 +285,9 @@ def records_from_json(text: str, images=None):
             r.x0, r.y0, r.x1, r.y1 = (float(s[k]) for k in ("x0", "y0", "x1", "y1"))
         elif t == "Cube":
             r.type = CUBE
+        elif t == "Torus":
+            r.type = TORUS
+            r.radius, r.tube_radius = float(s["radius"]), float(s["tube_radius"])
         elif t == "BruteForsableShape":
             fn = s["shape"]
             if fn["type"] not in FUNC_IDS:

@@ -279,6 +279,7 @@ typedef struct {
     mat4 direct, inverse;
     double x0, y0, x1, y1, step;
     double fa, fb, fc, fd, fr;
+    double radius, tube_radius;
 } shape_t;
 
 typedef struct {
@@ -412,6 +413,8 @@ or_scene *or_scene_new(const or_shape_in *shapes, int n, const or_material_in *m
         sh.fc = shapes[i].fc;
         sh.fd = shapes[i].fd;
         sh.fr = shapes[i].fr;
+        sh.radius = shapes[i].radius;
+        sh.tube_radius = shapes[i].tube_radius;
         transform_new(vload(shapes[i].translate), vload(shapes[i].rotate), vload(shapes[i].scale),
                       &sh.direct, &sh.inverse);
         push_shape(s, sh);
@@ -452,6 +455,8 @@ void or_scene_get_shape(const or_scene *s, int i, or_shape_out *o) {
     o->fc = sh->fc;
     o->fd = sh->fd;
     o->fr = sh->fr;
+    o->radius = sh->radius;
+    o->tube_radius = sh->tube_radius;
 }
 void or_scene_get_material(const or_scene *s, int i, or_material_in *o) {
     const mat_t *m = &s->mats[i];
@@ -719,14 +724,128 @@ done:
     return 1;
 }
 
+/* ---- Torus ------------------------------------------------------------- */
+/* num::Complex<f64> (num 0.4, unpinned release) as num-complex publishes it:
+ * Mul / Div by the textbook formulas (Div via norm_sqr), real operands
+ * componentwise, sqrt / cbrt special-cased on the axes (sign of a zero
+ * imaginary part picks the root), else from_polar(hypot, atan2). */
+typedef struct {
+    double re, im;
+} cplx;
+static cplx C2(double re, double im) { cplx z = {re, im}; return z; }
+static cplx c_add(cplx a, cplx b) { return C2(a.re + b.re, a.im + b.im); }
+static cplx c_sub(cplx a, cplx b) { return C2(a.re - b.re, a.im - b.im); }
+static cplx c_neg(cplx a) { return C2(-a.re, -a.im); }
+static cplx c_mul(cplx a, cplx b) { return C2(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re); }
+static cplx c_div(cplx a, cplx b) {
+    double n = b.re * b.re + b.im * b.im;
+    return C2((a.re * b.re + a.im * b.im) / n, (a.im * b.re - a.re * b.im) / n);
+}
+static cplx c_scale(double k, cplx a) { return C2(k * a.re, k * a.im); }  /* f64 * Complex */
+static cplx c_divr(cplx a, double k) { return C2(a.re / k, a.im / k); }   /* Complex / f64 */
+static int sign_positive(double x) { return !signbit(x); }
+static cplx c_polar(double r, double th) { return C2(r * cos(th), r * sin(th)); }
+static cplx c_sqrt(cplx z) {
+    if (z.im == 0.0) {
+        if (sign_positive(z.re)) return C2(sqrt(z.re), z.im);
+        double im = sqrt(-z.re);
+        return sign_positive(z.im) ? C2(0.0, im) : C2(0.0, -im);
+    }
+    if (z.re == 0.0) {
+        double x = sqrt(fabs(z.im) / 2.0);
+        return sign_positive(z.im) ? C2(x, x) : C2(x, -x);
+    }
+    return c_polar(sqrt(hypot(z.re, z.im)), atan2(z.im, z.re) / 2.0);
+}
+static cplx c_cbrt(cplx z) {
+    if (z.im == 0.0) {
+        if (sign_positive(z.re)) return C2(cbrt(z.re), z.im);
+        double re = cbrt(-z.re) / 2.0, im = sqrt(3.0) * re;
+        return sign_positive(z.im) ? C2(re, im) : C2(re, -im);
+    }
+    if (z.re == 0.0) {
+        double im = cbrt(fabs(z.im)) / 2.0, re = sqrt(3.0) * im;
+        return sign_positive(z.im) ? C2(re, im) : C2(re, -im);
+    }
+    return c_polar(cbrt(hypot(z.re, z.im)), atan2(z.im, z.re) / 3.0);
+}
+/* solve_quantic_equation: equation.rs:17-67 */
+static void quartic(cplx a, cplx b, cplx c, cplx d, cplx e, cplx out[4]) {
+    b = c_div(b, a);
+    c = c_div(c, a);
+    d = c_div(d, a);
+    e = c_div(e, a);
+    cplx b2 = c_mul(b, b);
+    cplx alpha = c_sub(c, c_scale(3.0 / 8.0, b2));
+    cplx beta = c_add(c_sub(c_divr(c_mul(b2, b), 8.0), c_divr(c_mul(b, c), 2.0)), d);
+    cplx gamma = c_add(c_sub(c_add(c_mul(c_scale(-3.0 / 256.0, b2), b2), c_divr(c_mul(b2, c), 16.0)),
+                             c_divr(c_mul(b, d), 4.0)), e);
+    cplx alpha2 = c_mul(alpha, alpha);
+    cplx t = c_divr(c_neg(b), 4.0);
+    if (approx_equal(beta.re, 0.0) && approx_equal(beta.im, 0.0)) {
+        cplx r = c_sqrt(c_sub(alpha2, c_scale(4.0, gamma)));
+        cplx r1 = c_sqrt(c_divr(c_add(c_neg(alpha), r), 2.0));
+        cplx r2 = c_sqrt(c_divr(c_sub(c_neg(alpha), r), 2.0));
+        out[0] = c_add(t, r1);
+        out[1] = c_sub(t, r1);
+        out[2] = c_add(t, r2);
+        out[3] = c_sub(t, r2);
+        return;
+    }
+    cplx p = c_neg(c_add(c_divr(alpha2, 12.0), gamma));
+    cplx q = c_sub(c_add(c_divr(c_mul(c_neg(alpha2), alpha), 108.0), c_divr(c_mul(alpha, gamma), 3.0)),
+                   c_divr(c_mul(beta, beta), 8.0));
+    cplx r = c_add(c_divr(c_neg(q), 2.0), c_sqrt(c_add(c_divr(c_mul(q, q), 4.0), c_divr(c_mul(c_mul(p, p), p), 27.0))));
+    cplx u = c_cbrt(r);
+    cplx y = c_add(c_scale(-5.0 / 6.0, alpha), u);
+    if (approx_equal(u.re, 0.0) && approx_equal(u.im, 0.0)) y = c_sub(y, c_cbrt(q));
+    else y = c_sub(y, c_div(p, c_scale(3.0, u)));
+    cplx w = c_sqrt(c_add(alpha, c_scale(2.0, y)));
+    cplx r1 = c_sqrt(c_neg(c_add(c_add(c_scale(3.0, alpha), c_scale(2.0, y)), c_div(c_scale(2.0, beta), w))));
+    cplx r2 = c_sqrt(c_neg(c_sub(c_add(c_scale(3.0, alpha), c_scale(2.0, y)), c_div(c_scale(2.0, beta), w))));
+    out[0] = c_add(t, c_divr(c_sub(w, r1), 2.0));
+    out[1] = c_add(t, c_divr(c_add(w, r1), 2.0));
+    out[2] = c_add(t, c_divr(c_sub(c_neg(w), r2), 2.0));
+    out[3] = c_add(t, c_divr(c_add(c_neg(w), r2), 2.0));
+}
+void or_solve_quartic(double a, double b, double c, double d, double e, double re[4], double im[4]) {
+    cplx out[4];
+    quartic(C2(a, 0.0), C2(b, 0.0), C2(c, 0.0), C2(d, 0.0), C2(e, 0.0), out);
+    for (int i = 0; i < 4; i++) {
+        re[i] = out[i].re;
+        im[i] = out[i].im;
+    }
+}
+/* Torus::ray_intersect distance: mod.rs:430-462 */
+static int torus_t(const shape_t *s, v3 o, v3 d, double min_t, double max_t, double *out) {
+    double R = s->radius, r = s->tube_radius;
+    double t = 4.0 * R * R;
+    double g = t * (d.x * d.x + d.y * d.y);
+    double h = 2.0 * t * (o.x * d.x + o.y * d.y);
+    double i = t * (o.x * o.x + o.y * o.y);
+    double j = vdot(d, d);
+    double k = 2.0 * vdot(o, d);
+    double l = vdot(o, o) + R * R - r * r;
+    cplx roots[4];
+    quartic(C2(j * j, 0.0), C2(2.0 * j * k, 0.0), C2(2.0 * j * l + k * k - g, 0.0), C2(2.0 * k * l - h, 0.0),
+            C2(l * l - i, 0.0), roots);
+    double m = INFINITY;
+    for (int q = 0; q < 4; q++)
+        if (approx_equal(roots[q].im, 0.0) && roots[q].re < m) m = roots[q].re;
+    if (isinf(m) || m < min_t || m > max_t) return 0;
+    *out = m;
+    return 1;
+}
+
 /* Object-space test dispatch. */
 static int shape_t_obj(const shape_t *s, v3 o, v3 d, double min_t, double max_t, double *t, or_stats *st) {
-    if (st && s->type >= 0 && s->type < 4) st->shape_tests[s->type]++;
+    if (st && s->type >= 0 && s->type < 4) st->shape_tests[s->type]++; /* (Torus tests are not counted) */
     switch (s->type) {
     case OR_SPHERE: return sphere_t(o, d, min_t, max_t, t);
     case OR_RECT: return rect_t(s, o, d, min_t, max_t, t);
     case OR_CUBE: return cube_t(o, d, min_t, max_t, t);
     case OR_MARCH: return march_t(s, o, d, min_t, max_t, t, st);
+    case OR_TORUS: return torus_t(s, o, d, min_t, max_t, t);
     }
     return 0;
 }
@@ -759,6 +878,11 @@ static v3 shape_obj_normal(const shape_t *s, v3 o, v3 d, double t, v3 *p_out) {
         *p_out = p;
         return func_gradient(s, p);
     }
+    case OR_TORUS: { /* mod.rs:464-465: p - normalize((p.x, p.y, 0)) * radius */
+        v3 p = vadd(o, vscale(d, t));
+        *p_out = p;
+        return vsub(p, vscale(vnorm(V(p.x, p.y, 0.0)), s->radius));
+    }
     }
     *p_out = V(NAN, NAN, NAN);
     return V(NAN, NAN, NAN);
@@ -789,6 +913,13 @@ static void shape_uv(const shape_t *s, v3 p, double *u, double *v) {
         else if (mc == pa.y) { *u = p.x; *v = p.z; }
         else if (mc == pa.z) { *u = p.x; *v = p.y; }
         else { *u = NAN; *v = NAN; }
+        return;
+    }
+    case OR_TORUS: { /* mod.rs:466-467 */
+        double theta = asin(p.z / s->tube_radius);
+        double phi = acos(p.z / (s->radius + s->tube_radius * cos(theta))) + M_PI;
+        *u = phi / (2.0 * M_PI);
+        *v = theta / M_PI;
         return;
     }
     default:
@@ -849,6 +980,12 @@ static void shape_bbox(const shape_t *s, v3 *mn, v3 *mx) {
             hi[0] = hi[1] = hi[2] = s->fr;
         }
         break;
+    case OR_TORUS: { /* mod.rs:478-485 */
+        double a = s->radius + s->tube_radius;
+        lo[0] = -a; lo[1] = -a; lo[2] = -s->tube_radius;
+        hi[0] = a; hi[1] = a; hi[2] = s->tube_radius;
+        break;
+    }
     default: lo[0] = lo[1] = lo[2] = -1.0; hi[0] = hi[1] = hi[2] = 1.0; break;
     }
     double omn[3], omx[3];

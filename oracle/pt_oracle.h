@@ -35,6 +35,7 @@ extern "C" {
 #define OR_RECT 1
 #define OR_CUBE 2
 #define OR_MARCH 3
+#define OR_TORUS 4
 
 /* ray-marched implicit functions (src/world/shapes/ray_marching.rs) */
 #define OR_FUNC_HEART 0
@@ -57,6 +58,7 @@ typedef struct {
     double translate[3], rotate[3], scale[3];
     double x0, y0, x1, y1, step;
     double fa, fb, fc, fd, fr; /* ray-marched function: a, b, c, d, sphere_radius */
+    double radius, tube_radius; /* Torus */
 } or_shape_in;
 
 /* textures (src/world/texture.rs) */
@@ -86,6 +88,7 @@ typedef struct {
     double direct[16], inverse[16];
     double x0, y0, x1, y1, step;
     double fa, fb, fc, fd, fr;
+    double radius, tube_radius;
 } or_shape_out;
 
 typedef struct {
@@ -163,6 +166,10 @@ uint64_t or_rng_next(uint64_t *state);
 double or_gen_f64(uint64_t *state);
 double or_uniform_incl_scale(double lo, double hi);
 double or_gen_range_incl(uint64_t *state, double lo, double hi);
+
+/* ---- Torus (src/world/shapes/mod.rs:429-476; algebra/equation.rs:17-67) --- */
+/* solve_quantic_equation on real coefficients: roots re[4], im[4] in its order */
+void or_solve_quartic(double a, double b, double c, double d, double e, double re[4], double im[4]);
 
 /* ---- path -------------------------------------------------------------- */
 int or_shape_hit(const or_scene *s, int shape, const double o[3], const double d[3], double min_t,

@@ -31,7 +31,7 @@ LIB_PATH = PKG_DIR / "librs_pathtracing_amd.so"
 
 PT_OK = 0
 PT_ERR_INVALID, PT_ERR_PARSE, PT_ERR_UNSUPPORTED, PT_ERR_HIP, PT_ERR_STATE = -1, -2, -3, -4, -5
-SPHERE, RECTANGLE, CUBE, MARCH = 0, 1, 2, 3
+SPHERE, RECTANGLE, CUBE, MARCH, TORUS = 0, 1, 2, 3, 4
 LAMBERTIAN, METAL, DIELECTRIC, DIFFUSE_LIGHT, EMPTY = 0, 1, 2, 3, 4
 TILE = 16
 
@@ -74,7 +74,7 @@ class ShapeInfo(C.Structure):
                 ("direct", C.c_double * 16), ("inverse", C.c_double * 16),
                 ("x0", C.c_double), ("y0", C.c_double), ("x1", C.c_double), ("y1", C.c_double),
                 ("step", C.c_double), ("a", C.c_double), ("b", C.c_double), ("c", C.c_double), ("d", C.c_double),
-                ("sphere_radius", C.c_double)]
+                ("sphere_radius", C.c_double), ("radius", C.c_double), ("tube_radius", C.c_double)]
 
 
 class MaterialInfo(C.Structure):
@@ -357,7 +357,7 @@ class HipRenderer(Renderer):
 
 COUNTERS = ["samples", "bounces", "test_sphere", "test_rect", "test_cube", "test_march", "node_slabs",
             "march_slabs", "march_steps", "march_tries", "march_blocks", "hits", "lambert", "metal",
-            "dielectric", "reject_tries", "unwind"]
+            "dielectric", "reject_tries", "unwind", "test_torus"]
 
 
 def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,

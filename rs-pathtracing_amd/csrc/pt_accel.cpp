@@ -29,6 +29,12 @@ DBox shape_box(const HostShape &s) {
             hi[0] = hi[1] = hi[2] = r;
         }
         break;
+    case TORUS: {  // get_bounding_box (mod.rs:478-485)
+        const double a = s.radius + s.tube_radius;
+        lo[0] = -a; lo[1] = -a; lo[2] = -s.tube_radius;
+        hi[0] = a; hi[1] = a; hi[2] = s.tube_radius;
+        break;
+    }
     default:
         lo[0] = lo[1] = lo[2] = -1.0;
         hi[0] = hi[1] = hi[2] = 1.0;
@@ -121,7 +127,10 @@ Accel build_accel(const Scene &sc, int json_shapes) {
     bool small = json_shapes <= LIN_MAX;
     for (int32_t i = 0; i < (int32_t)sc.shapes.size(); i++) {
         if (sc.shapes[i].type == MARCH) a.march.push_back(i);
-        else if (small && i < json_shapes) a.lin.push_back(i);
+        // a Torus root comes from a closed-form quartic whose error has no
+        // useful bound: never behind a box (the acceptance rule keeps the
+        // linear scan's result in any visiting order)
+        else if ((small && i < json_shapes) || sc.shapes[i].type == TORUS) a.lin.push_back(i);
         else rest.push_back(i);
     }
     if (!rest.empty()) {

@@ -6,7 +6,8 @@
 // into three groups, all tested with one acceptance rule — accept t if
 // t < best or (t == best and shape index > best index) — which reproduces the
 // linear scan's "later shape wins a tie" in any visiting order:
-//   * `lin`   — the JSON shapes when there are few: a wave-uniform loop;
+//   * `lin`   — the JSON shapes when there are few, and every Torus: a
+//               wave-uniform loop;
 //   * BVH     — everything else that is not ray-marched (random spheres,
 //               large scenes), median-split, threaded, padded f64 boxes;
 //   * `march` — ray-marched shapes, tested last behind their padded box

@@ -146,6 +146,8 @@ int pt_scene_get_shape(const pt_scene *s, int i, pt_shape_info *o) {
     o->c = h.fc;
     o->d = h.fd;
     o->sphere_radius = h.fr;
+    o->radius = h.radius;
+    o->tube_radius = h.tube_radius;
     return PT_OK;
 }
 int pt_scene_get_material(const pt_scene *s, int i, pt_material_info *o) {
@@ -225,6 +227,9 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     r->ds.nnodes = (int)acc.nodes.size();
     r->ds.nlin = (int)acc.lin.size();
     r->ds.nmarch = (int)acc.march.size();
+    r->ds.ext = S.textures.empty() ? 0 : 1;
+    for (const auto &h : S.shapes)
+        if (h.type == TORUS) r->ds.ext = 1;
     r->ds.fkind = 0;  // Heart-only kernel builds unless another function is marched
     for (const auto &h : r->scene->s.shapes)
         if (h.type == MARCH && h.func != 0) r->ds.fkind = -1;

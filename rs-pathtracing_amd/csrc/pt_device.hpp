@@ -12,6 +12,7 @@
 #include <cstdint>
 
 #include "pt_march.hpp"
+#include "pt_torus.hpp"
 #include "pt_types.hpp"
 
 namespace pt {
@@ -159,9 +160,11 @@ struct Ray {
 #endif
 // MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
 // every one on the march list), so the march branch is not compiled in.
-template <bool STATS, int FK = march::F_ANY, bool MARCHED = true>
+// EXT: the extended build (scenes with a Torus or non-solid textures) that
+// also carries the Torus' quartic; other builds never see a Torus.
+template <bool STATS, int FK = march::F_ANY, bool MARCHED = true, bool EXT = false>
 PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct) {
-    if (STATS) ct->c[C_TEST_SPHERE + s.type]++;
+    if (STATS) ct->c[s.type == TORUS ? C_TEST_TORUS : C_TEST_SPHERE + s.type]++;
     if (PT_LAZY_RECT && s.type == RECTANGLE) {
         // Rectangle: t needs only the object-space z row; x and y are
         // transformed only for a t in range.  Each component is the same
@@ -186,6 +189,9 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
     case SPHERE: return sphere_t(o, d, min_t, max_t, t);
     case RECTANGLE: return rect_t(s.p, o, d, min_t, max_t, t);
     case CUBE: return cube_t(o, d, min_t, max_t, t);
+    case TORUS:
+        if (!EXT) return false;
+        return torus::torus_t(s.p[0], s.p[1], o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t, t);
     default: {
         if (!MARCHED) return false;
         march::MarchStats ms{0, 0, 0};
@@ -255,6 +261,7 @@ struct Scene {
     const DImage *__restrict__ images;
     const uint8_t *__restrict__ pixels;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
+    int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
 };
 
 // Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
@@ -273,7 +280,7 @@ PT_HD bool slab(const double *lo, const double *hi, const Ray &r, V3 inv, double
 // in the shape list — the linear scan's "later shape wins a tie" rule, which
 // makes the visiting order (uniform list, BVH, marched shapes last) irrelevant.
 // This part covers the uniform list and the BVH; marched shapes follow.
-template <bool STATS = false>
+template <bool STATS = false, bool EXT = false>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
                            Ctr *ct = nullptr) {
     double best = *best_t;
@@ -283,7 +290,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
         const int i = uniform_load(&sc.lin[k]);
         const DShape s = uniform_shape(&sc.shapes[i]);
         double t;
-        if (shape_test<STATS, march::F_ANY, false>(s, r, min_t, best, &t, ct) && (t < best || i > who)) {
+        if (shape_test<STATS, march::F_ANY, false, EXT>(s, r, min_t, best, &t, ct) && (t < best || i > who)) {
             best = t;
             who = i;
         }
@@ -311,12 +318,12 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     *who_out = who;
 }
 
-template <bool STATS = false>
+template <bool STATS = false, bool EXT = false>
 PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, double *best_t, Ctr *ct = nullptr) {
     double best = max_t;
     int who = -1;
     V3 inv = v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
-    closest_nomarch<STATS>(sc, r, inv, min_t, &best, &who, ct);
+    closest_nomarch<STATS, EXT>(sc, r, inv, min_t, &best, &who, ct);
     // ray-marched shapes last, only if their padded box is entered before `best`
     for (int k = 0; k < ((sc.diag & 1) ? 0 : sc.nmarch); k++) {
         int i = sc.march[k];
@@ -357,6 +364,9 @@ PT_HD Hit finish(const DShape &s, const Ray &r, double t) {
         else n = v3(__builtin_nan(""), __builtin_nan(""), __builtin_nan(""));
         break;
     }
+    case TORUS:  // mod.rs:465: p - normalize((p.x, p.y, 0)) * radius
+        n = sub(p, scale(normalize(v3(p.x, p.y, 0.0)), s.p[0]));
+        break;
     default: {  // ray_marching.rs:59-60: the function's gradient at p
         double g[3];
         march::shape_gradient_k<FK>(shape_params(s), p.x, p.y, p.z, g);
@@ -402,6 +412,13 @@ PT_HD void hit_uv(const DShape &s, const Ray &r, double t, double *u, double *v)
         else if (mc == ay) *u = p.x, *v = p.z;
         else if (mc == az) *u = p.x, *v = p.y;
         else *u = *v = __builtin_nan("");
+        return;
+    }
+    case TORUS: {  // mod.rs:466-467
+        const double theta = asin(p.z / s.p[1]);
+        const double phi = acos(p.z / (s.p[0] + s.p[1] * cos(theta))) + PI;
+        *u = phi / (2.0 * PI);
+        *v = theta / PI;
         return;
     }
     default:
@@ -581,9 +598,9 @@ struct IdStack {
 // Everything in a bounce after the closest hit (who, t) is known.
 // Stack: any type with push(id), pop() and a count n (IdStack in registers,
 // or the wavefront engine's per-slot id array in HBM).
-// TEX: the build for scenes with non-solid textures (textured albedos are
+// EXT: the build for scenes with non-solid textures or a Torus (textured albedos are
 // evaluated at the hit and pushed by value; textured lights emit their value).
-template <bool STATS = false, int FK = march::F_ANY, bool TEX = false, class Stack>
+template <bool STATS = false, int FK = march::F_ANY, bool EXT = false, class Stack>
 PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, Stack &stk, Rng &rng,
                  double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
@@ -611,13 +628,13 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         V3 u = normalize(random_in_unit_sphere<STATS>(rng, s11, ct));
         dir = add(h.n, u);
         if (approx_zero(dir.x) && approx_zero(dir.y) && approx_zero(dir.z)) dir = h.n;
-        if (TEX && m.tex >= 0) stk.push_val(textured());
+        if (EXT && m.tex >= 0) stk.push_val(textured());
         else stk.push((uint32_t)s.material);
     } else if (m.type == METAL) {  // :63-76
         if (STATS) ct->c[C_METAL]++;
         V3 rf = reflect(ray.d, h.n);
         dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
-        if (TEX && m.tex >= 0) stk.push_val(textured());
+        if (EXT && m.tex >= 0) stk.push_val(textured());
         else stk.push((uint32_t)s.material);
     } else if (m.type == DIELECTRIC) {  // :92-115
         if (STATS) ct->c[C_DIELECTRIC]++;
@@ -634,7 +651,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         }
         dir = refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio);
     } else {  // DiffuseLight / EmptyMaterial: no scatter, emitted()
-        if (TEX && m.type == DIFFUSE_LIGHT && m.tex >= 0) *leaf = textured();
+        if (EXT && m.type == DIFFUSE_LIGHT && m.tex >= 0) *leaf = textured();
         else *leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
         return true;
     }
@@ -644,21 +661,21 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     return false;
 }
 
-template <int NW, bool STATS = false, bool TEX = false>
+template <int NW, bool STATS = false, bool EXT = false>
 PT_HD bool bounce(const Scene &sc, Ray &ray, uint32_t &depth, IdStack<NW> &stk, Rng &rng, double s11, V3 *leaf,
                   Ctr *ct = nullptr) {
     double t;
     if (STATS) ct->c[C_BOUNCES]++;
-    int who = closest<STATS>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
-    return shade<STATS, march::F_ANY, TEX>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
+    int who = closest<STATS, EXT>(sc, ray, T_MIN, __builtin_inf(), &t, ct);
+    return shade<STATS, march::F_ANY, EXT>(sc, who, t, ray, depth, stk, rng, s11, leaf, ct);
 }
 
-template <bool STATS = false, bool TEX = false, class Stack>
+template <bool STATS = false, bool EXT = false, class Stack>
 PT_HD V3 unwind(const Scene &sc, Stack &stk, V3 c, Ctr *ct = nullptr) {
     while (stk.n > 0) {
         if (STATS) ct->c[C_UNWIND]++;
         const uint32_t id = stk.pop();
-        if (TEX && (id & VAL_BIT)) {
+        if (EXT && (id & VAL_BIT)) {
             const V3 a = stk.val(stk.n);
             c = v3(a.x * c.x, a.y * c.y, a.z * c.z);
         } else {
@@ -670,8 +687,8 @@ PT_HD V3 unwind(const Scene &sc, Stack &stk, V3 c, Ctr *ct = nullptr) {
 }
 
 // ray_color (src/renderer/mod.rs:23-45), iterative with the recursion's product order.
-// vb, vs: the textured-attenuation area of this lane (TEX builds).
-template <int NW, bool TEX = false>
+// vb, vs: the textured-attenuation area of this lane (EXT builds).
+template <int NW, bool EXT = false>
 PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s11, double *vb = nullptr,
                    size_t vs = 0) {
     IdStack<NW> stk;
@@ -679,9 +696,9 @@ PT_HD V3 ray_color(const Scene &sc, Ray ray, uint32_t depth, Rng &rng, double s1
     stk.vb = vb;
     stk.vs = vs;
     V3 leaf;
-    while (!bounce<NW, false, TEX>(sc, ray, depth, stk, rng, s11, &leaf)) {
+    while (!bounce<NW, false, EXT>(sc, ray, depth, stk, rng, s11, &leaf)) {
     }
-    return unwind<false, TEX>(sc, stk, leaf);
+    return unwind<false, EXT>(sc, stk, leaf);
 }
 
 // Camera sample: MultisamplerRayCaster::next (ray_caster.rs:103-118), u then v.
@@ -714,7 +731,7 @@ constexpr int MARCH_ITERS = 2;  // march iterations per pass of the loop
 enum Phase : int { PH_TRACE = 0, PH_SELECT = 1, PH_MARCH = 2, PH_SHADE = 3 };
 
 
-template <int NW, bool STATS = false, bool TIMING = false, int FK = march::F_ANY, bool TEX = false>
+template <int NW, bool STATS = false, bool TIMING = false, int FK = march::F_ANY, bool EXT = false>
 PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t y, Ctr *ct = nullptr,
                      PhaseTimes *pt = nullptr, double *vb = nullptr, size_t vs = 0) {
     uint64_t pixel = (uint64_t)x + (uint64_t)y * P.width;
@@ -744,7 +761,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
             inv = v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             best = __builtin_inf();
             who = -1;
-            closest_nomarch<STATS>(sc, ray, inv, T_MIN, &best, &who, ct);
+            closest_nomarch<STATS, EXT>(sc, ray, inv, T_MIN, &best, &who, ct);
             km = 0;
             phase = PH_SELECT;
         }
@@ -798,7 +815,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_SHADE) {
             V3 leaf;
             uint64_t tf = 0;
-            const bool ended = shade<STATS, FK, TEX>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
+            const bool ended = shade<STATS, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf, ct,
                                                      TIMING ? &tf : nullptr);
             if (TIMING) {
                 uint64_t n = PT_STAMP();
@@ -809,7 +826,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
                 ts = n;
             }
             if (ended) {
-                acc = add(acc, unwind<STATS, TEX>(sc, stk, leaf, ct));
+                acc = add(acc, unwind<STATS, EXT>(sc, stk, leaf, ct));
                 if (STATS) ct->c[C_SAMPLES]++;
                 if (++s == P.spp) break;
                 rng.s = sample_key(P.seed, pixel, s);

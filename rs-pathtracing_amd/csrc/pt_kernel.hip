@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void closest_hit_probe(dev::Scene sc, const do
     r.o = dev::v3(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
     r.d = dev::v3(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
     double t;
-    int who = dev::closest(sc, r, min_t, max_t, &t);
+    int who = dev::closest<false, true>(sc, r, min_t, max_t, &t);
     pt_hit h = {};
     h.shape = who;
     h.material = -1;
@@ -212,6 +212,7 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.perlin = s.perlin;
     d.images = s.images;
     d.pixels = s.pixels;
+    d.ext = s.ext;
     d.nnodes = s.nnodes;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
@@ -257,7 +258,7 @@ hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double
                               WaveWorkspace *ws, int fkind);
 
 static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
-    if (s.tex) return true;  // textured scenes: the megakernel keeps attenuation ids in registers only
+    if (s.ext) return true;  // textures / Torus: the extended builds live in the wavefront engine
     const char *e = getenv("PT_ENGINE");
     if (e && e[0] == 'm') return false;
     if (e && e[0] == 'w') return ws != nullptr;
@@ -312,7 +313,7 @@ struct ProbeVals {
     double *p = nullptr;
     hipStream_t st;
     hipError_t alloc(const DeviceScene &s, size_t n, uint32_t depth) {
-        if (!s.tex) return hipSuccess;
+        if (!s.ext) return hipSuccess;
         return hipMallocAsync((void **)&p, n * (depth + 1) * 3 * sizeof(double), st);
     }
     ~ProbeVals() {
@@ -363,7 +364,7 @@ hipError_t launch_march_probe(const double *jobs, size_t n, double *t, int32_t *
 hipError_t launch_render_timed(const DeviceScene &s, const FrameParams &P, double *out, unsigned long long *acc,
                                hipStream_t st) {
     if (P.tile_count == 0) return hipSuccess;
-    if (s.tex) return hipErrorNotSupported;  // the timing build has no textured attenuation store
+    if (s.ext) return hipErrorNotSupported;  // the timing build has no extended (texture / Torus) build
     render_tiles_timed<<<P.tile_count, 256, 0, st>>>(dscene(s), P, out, acc);
     return hipGetLastError();
 }

@@ -214,6 +214,9 @@ DShape to_device(const HostShape &s) {
         d.p[1] = s.y0;
         d.p[2] = s.x1;
         d.p[3] = s.y1;
+    } else if (s.type == TORUS) {
+        d.p[0] = s.radius;
+        d.p[1] = s.tube_radius;
     } else if (s.type == MARCH) {
         d.p[0] = s.step;
         // constants shape_func computes from the parameters (pure, so the
@@ -623,8 +626,13 @@ Scene scene_from_json(const char *json, size_t len, bool random_spheres, uint64_
             }
             h.type = MARCH;
             h.material = mat_of(s);
-        } else if (t == "Torus") {
-            unsupported("shape `Torus` is not implemented on the GPU path");
+        } else if (t == "Torus") {  // shapes/mod.rs:766-789
+            str(field(s, "name"), "name");
+            h.radius = num(field(s, "radius"), "radius");
+            h.tube_radius = num(field(s, "tube_radius"), "tube_radius");
+            transform(field(s, "transform"), h);
+            h.type = TORUS;
+            h.material = mat_of(s);
         } else {
             schema("unknown variant `" + t + "` of ShapeJson");
         }

@@ -16,6 +16,7 @@ struct HostShape {
     int32_t type = 0, material = 0, inverse_normal = 0, depth = 4, func = 0;
     double direct[4][4], inverse[4][4];
     double x0 = 0, y0 = 0, x1 = 0, y1 = 0, step = 0;
+    double radius = 0, tube_radius = 0;  // Torus
     // RayMarchingShape function parameters as in the JSON (a, b, c, d,
     // sphere_radius; unused ones 0) and the derived constants the kernels use
     double fa = 0, fb = 0, fc = 0, fd = 0, fr = 0;

@@ -7,13 +7,13 @@
 
 namespace pt {
 
-enum ShapeKind : int32_t { SPHERE = 0, RECTANGLE = 1, CUBE = 2, MARCH = 3 };
+enum ShapeKind : int32_t { SPHERE = 0, RECTANGLE = 1, CUBE = 2, MARCH = 3, TORUS = 4 };
 enum MaterialKind : int32_t { LAMBERTIAN = 0, METAL = 1, DIELECTRIC = 2, DIFFUSE_LIGHT = 3, EMPTY = 4 };
 
 struct alignas(64) DShape {
     double inv[12];  // InversableTransform::inverse, rows 0..2 (3x4)
     double dir[12];  // InversableTransform::direct, rows 0..2
-    double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step
+    double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step | Torus radius, tube_radius
     int32_t type, material, inverse_normal, depth;
     int32_t func, pad[3];
     double fk[4];    // RayMarchingShape function constants (pt_funcs.hpp FParams::k)
@@ -80,7 +80,7 @@ struct FrameParams {
 enum Counter : int {
     C_SAMPLES, C_BOUNCES, C_TEST_SPHERE, C_TEST_RECT, C_TEST_CUBE, C_TEST_MARCH, C_NODE_SLABS, C_MARCH_SLABS,
     C_MARCH_STEPS, C_MARCH_TRIES, C_MARCH_BLOCKS, C_HITS, C_LAMBERT, C_METAL, C_DIELECTRIC, C_REJECT_TRIES,
-    C_UNWIND, C_COUNT
+    C_UNWIND, C_TEST_TORUS, C_COUNT
 };
 struct Ctr {
     uint64_t c[C_COUNT];

@@ -50,7 +50,7 @@ struct WfView {
     int32_t *who;    // best hit shape (-1: miss)
     uint32_t *meta;  // depth | stack count << 8
     uint32_t *ids;   // attenuation-id stack: entry k of a path at ids[k * cap + id]
-    double *att;     // textured attenuation values (TEX builds): (k * 3 + c) * cap + id
+    double *att;     // textured attenuation values (EXT builds): (k * 3 + c) * cap + id
     double *rx, *ry, *rz;  // sample radiance of finished paths
     uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
     uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
@@ -117,7 +117,7 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
 // DIAG: wave-level s_memtime cycles per section (load + shade, trace,
 // march pre-check, stores) summed into diag[36..39] (tuning only).
-template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool TEX = false>
+template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -160,10 +160,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
-                if (TEX) stk.vb = v.att + id;
+                if (EXT) stk.vb = v.att + id;
                 V3 leaf;
-                if (dev::shade<false, FK, TEX>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
-                    const V3 c = dev::unwind<false, TEX>(sc, stk, leaf);
+                if (dev::shade<false, FK, EXT>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                    const V3 c = dev::unwind<false, EXT>(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
                     v.rz[id] = c.z;
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
-            dev::closest_nomarch(sc, ray, inv, T_MIN, &best, &who);
+            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
             PT_BSTAMP(1)
             // does any marched shape's bound start before the best hit? (the
             // march kernel repeats this select and marches)
@@ -623,7 +623,7 @@ static int bounce_waves() {
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
                           const WfView &v, int it, unsigned long long *diag, int fkind) {
-    if (sc.tex) {  // non-solid textures: the generic textured build
+    if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
         wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
     }

@@ -198,6 +198,35 @@ def noise():
     }
 
 
+def torus():
+    """Tori (src/world/shapes/mod.rs:400-494; no reference scene uses one): a
+    lying ring, a standing UV-checked ring and a glass one over a ground."""
+    def ring(name, t, r, scale, mat, R=1.0, tube=0.3):
+        return {"type": "Torus", "name": name, "radius": R, "tube_radius": tube,
+                "transform": tr(t, r, (scale, scale, scale)), "material": mat}
+    return {
+        "camera": {"position": [0, 3, -10], "direction": [0, -0.25, 1], "up": [0, 1, 0], "fov": 35,
+                   "focal_length": 1},
+        "shapes": [
+            {"type": "Sphere", "name": "Ground", "transform": tr((0, -1000, 0), s=(1000, 1000, 1000)),
+             "material": "Ground"},
+            ring("Flat", (-2.5, 0.3, 0), (90, 0, 0), 1.0, "Copper"),
+            ring("Standing", (0, 1.3, 0.5), (0, 30, 0), 1.0, "UV", R=1.0, tube=0.25),
+            ring("Glassy", (2.6, 0.6, -0.5), (60, -20, 0), 0.8, "Glass", R=0.9, tube=0.35),
+            {"type": "Rectangle", "x0": -3, "x1": 3, "y0": -2, "y1": 2, "transform": tr((0, 7, 0), (90, 0, 0)),
+             "material": "Light"},
+        ],
+        "materials": {
+            "Ground": lambert((0.5, 0.55, 0.5)),
+            "Copper": {"type": "Metal", "albedo": solid((0.8, 0.5, 0.3)), "fuzz": 0.1},
+            "UV": {"type": "Lambertian", "albedo": uvchecker((0.9, 0.9, 0.2), (0.2, 0.3, 0.9), (16, 16))},
+            "Glass": {"type": "Dielectric", "index_of_refraction": 1.5},
+            "Light": {"type": "DiffuseLight", "emit": solid((5, 5, 5))},
+        },
+        "background": [0, 0, 0],
+    }
+
+
 def grid_ppm(w=64, h=32):
     """A small RGB test image (binary PPM): a colour ramp with a grid, so that
     every texel of an image-mapped sphere is distinguishable."""
@@ -253,6 +282,7 @@ def main():
     (HERE / "marched.json").write_text(json.dumps(marched(), indent=1) + "\n")
     (HERE / "textured.json").write_text(json.dumps(textured(), indent=1) + "\n")
     (HERE / "noise.json").write_text(json.dumps(noise(), indent=1) + "\n")
+    (HERE / "torus.json").write_text(json.dumps(torus(), indent=1) + "\n")
     (HERE / "textures").mkdir(exist_ok=True)
     (HERE / "textures" / "grid.ppm").write_bytes(grid_ppm())
     if a.synthetic:

@@ -385,8 +385,11 @@ TEX_CLOSE_MIN = 0.998
 
 
 @pytest.mark.parametrize("name,seed,depth", [("textured.json", 1, 8), ("noise.json", 2, 8),
-                                             ("textured.json", 3, 50)])
+                                             ("textured.json", 3, 50), ("torus.json", 2, 8)])
 def test_textured_frames(pt, name, seed, depth, monkeypatch):
+    """Textured scenes and the Torus (extended builds).  The Torus' quartic
+    (equation.rs:17-67) runs through hypot / atan2 / sin / cos / cbrt, so it
+    shares the texture tolerance."""
     from conftest import ROOT, scene_text
     monkeypatch.chdir(ROOT)
     text = scene_text(name)

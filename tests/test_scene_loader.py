@@ -86,8 +86,8 @@ def test_errors(pt):
     expect(pt, js, pt.PT_ERR_PARSE)
     js = base_scene()
     js["shapes"][0]["type"] = "Torus"
-    js["shapes"][0].update(radius=1, tube_radius=0.2)
-    expect(pt, js, pt.PT_ERR_UNSUPPORTED)
+    js["shapes"][0].update(radius=1)  # tube_radius is required
+    assert "tube_radius" in expect(pt, js, pt.PT_ERR_PARSE)
     js = base_scene()
     js["materials"]["M"]["albedo"] = {"type": "NoiseTexture"}  # `scale` is required
     assert "scale" in expect(pt, js, pt.PT_ERR_PARSE)

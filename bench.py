@@ -53,9 +53,30 @@ def flops_per_sample(cnt, keys=None):
     return sum(FLOP_WEIGHTS[k] * cnt[k] for k in keys) / max(1, cnt["samples"])
 
 
+# BASELINE.json configs[1..4] (configs[0] is the reference's own CPU case):
+# scene, width, height, spp.  c2 is the headline (the default); c5's scene is
+# generated (scenes/make_scenes.py synthetic(100000)), not a file.
+CONFIGS = {
+    "c2": ("cornell_box.json", 1920, 1080, 256),
+    "c3": ("cornell_box.json", 3840, 2160, 1024),
+    "c4": ("cornell_box.json", 3840, 2160, 4096),
+    "c5": ("synthetic_100000", 1920, 1080, 256),
+}
+
+
+def scene_text(name):
+    if name.startswith("synthetic_"):
+        sys.path.insert(0, str(ROOT / "scenes"))
+        import make_scenes
+        return json.dumps(make_scenes.synthetic(int(name.split("_")[1])))
+    return (ROOT / "scenes" / name).read_text()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="a BASELINE.json config (default: c2 through the flags below)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="cornell_box.json")
@@ -69,7 +90,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--parity-pixels", type=int, default=48)
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config:
+        a.scene, a.width, a.height, a.spp = CONFIGS[a.config]
+    return a
 
 
 def cpu_baseline(text, args, threads):
@@ -121,7 +145,7 @@ def main():
 
     import __graft_entry__ as ge
     pt = ge.load_package()
-    text = (ROOT / "scenes" / args.scene).read_text()
+    text = scene_text(args.scene)
     scene = pt.Scene.from_json(text, seed=args.scene_seed)
     r = pt.HipRenderer(scene, device=local, depth=args.depth)
     cam = scene.camera()
@@ -202,7 +226,7 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: re-authored cornell_box.json, add_random_spheres from seed %d" % args.scene_seed,
+            "data": "synthetic: re-authored %s, add_random_spheres from seed %d" % (args.scene, args.scene_seed),
             "config": {"workload": "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth),
                        "width": W, "height": H, "spp": spp, "depth": args.depth, "seed": args.seed,
                        "parallelism": "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"},

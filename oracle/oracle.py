@@ -328,8 +328,8 @@ class Scene:
         self.n_json_shapes = n
 
     def __del__(self):
-        if getattr(self, "ptr", None):
-            lib().or_scene_free(self.ptr)
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.or_scene_free(self.ptr)
             self.ptr = None
 
     def use_bvh(self, enable: bool = True, seed: int = 7):

@@ -210,6 +210,122 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         for (int k = 0; k < 4; k++) atomicAdd(&diag[36 + k], dsec[k]);
 }
 
+// Fused bounces (the default engine step): a lane carries its path through as
+// many bounces as it can without a march — shade the pending hit, trace the
+// new ray, and if no marched shape's bound starts before the best hit, shade
+// that hit at once in registers and go on.  Path state goes to HBM only when
+// the path needs a march (status 3: it joins the march queue and, after the
+// march, the next iteration's live list) or ends (its sample radiance).  The
+// grid is persistent: lanes whose path is done take the next path from the
+// block's runs of the input list (runs of `slice` ids dealt round-robin to the
+// blocks, an LDS head), so long paths do not hold finished lanes idle.  The
+// per-path sequence of operations is wf_bounce's, so the frame is the same
+// bit for bit; only paths that never meet a march skip the per-bounce state
+// round trip through HBM and the per-bounce launch.
+template <bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false>
+__global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParams P, WfView v, int it,
+                                                       uint32_t slice) {
+    __shared__ uint32_t head;
+    const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
+    const uint32_t G = gridDim.x;
+    const uint32_t runs = (count + slice - 1) / slice;
+    const uint32_t per = (runs > blockIdx.x ? (runs - blockIdx.x + G - 1) / G : 0u) * slice;
+    auto pos = [&](uint32_t q) -> uint32_t { return (q / slice * G + blockIdx.x) * slice + q % slice; };
+    if (threadIdx.x == 0) head = blockDim.x;
+    __syncthreads();
+    uint32_t q = threadIdx.x;
+    bool have = q < per && pos(q) < count;
+    bool fresh = true;
+    uint32_t id = 0, depth = 0;
+    Ray ray;
+    ray.o = ray.d = dev::v3(0.0, 0.0, 0.0);
+    dev::Rng rng{0};
+    MemStack stk{v.ids, (size_t)v.cap, 0, nullptr};
+    double best = 0.0;
+    int who = -1;
+    while (have) {
+        bool done = false, shade_now = true;
+        if (fresh) {
+            fresh = false;
+            if (FIRST) {
+                shade_now = false;
+                id = pos(q);
+                uint32_t x, y, sl, pl;
+                slot_pixel(P, v, id, &x, &y, &sl, &pl);
+                if (x >= P.width || y >= P.height || sl >= v.ns) {
+                    v.status[id] = 0;
+                    done = true;
+                } else {
+                    rng.s = dev::sample_key(P.seed, (uint64_t)x + (uint64_t)y * P.width, v.s0 + sl);
+                    ray = dev::camera_ray(P, x, y, rng);
+                    depth = P.depth;
+                    stk.base = v.ids + id;
+                    stk.n = 0;
+                    if (EXT) stk.vb = v.att + id;
+                }
+            } else {
+                id = v.list[pos(q)];
+                ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
+                ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
+                rng.s = v.rng[id];
+                const uint32_t meta = v.meta[id];
+                depth = meta & 0xffu;
+                stk.base = v.ids + id;
+                stk.n = (int)(meta >> 8);
+                if (EXT) stk.vb = v.att + id;
+                who = v.who[id];
+                best = v.t[id];
+            }
+        }
+        if (!done && shade_now) {
+            V3 leaf;
+            if (dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf)) {
+                const V3 c = dev::unwind<false, EXT>(sc, stk, leaf);
+                v.rx[id] = c.x;
+                v.ry[id] = c.y;
+                v.rz[id] = c.z;
+                v.status[id] = 0;
+                done = true;
+            }
+        }
+        if (!done) {
+            const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+            best = __builtin_inf();
+            who = -1;
+            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
+            bool need_march = false;
+            for (int k = 0; k < sc.nmarch && !need_march; k++) {
+                const int s = dev::uniform_load(&sc.march[k]);
+                const DBox b = dev::uniform_box(&sc.boxes[s]);
+                if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
+                const DShape S = dev::uniform_shape(&sc.shapes[s]);
+                const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
+                double st, en;
+                need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
+            }
+            if (need_march) {
+                v.ox[id] = ray.o.x;
+                v.oy[id] = ray.o.y;
+                v.oz[id] = ray.o.z;
+                v.dx[id] = ray.d.x;
+                v.dy[id] = ray.d.y;
+                v.dz[id] = ray.d.z;
+                v.t[id] = best;
+                v.who[id] = who;
+                v.rng[id] = rng.s;
+                v.meta[id] = depth | ((uint32_t)stk.n << 8);
+                v.status[id] = 3;
+                done = true;
+            }
+        }
+        if (done) {
+            q = atomicAdd(&head, 1u);
+            have = q < per && pos(q) < count;
+            fresh = true;
+        }
+    }
+}
+
 // Order-preserving compaction of the status bytes into the two id lists
 // (live paths: bit 0, march jobs: bit 1) in three small launches: per-tile
 // counts (16 statuses per thread, one 16-byte load), one scan over the tile
@@ -649,6 +765,51 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
     }
 }
 
+// Exactly the resident blocks of one kernel build (persistent grids).
+template <class K>
+static uint32_t resident_blocks(K kern) {
+    int dev = 0, cus = 256, occ = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1) occ = 1;
+    return (uint32_t)(cus * occ);
+}
+
+// The fused bounce step (wf_trace) unless PT_WF_FUSED=0 in the environment
+// (read per render: one wf_bounce launch per bounce, the engine before fusion,
+// kept for A/B tests; the diag build always runs wf_bounce).
+static bool fused_bounces() {
+    const char *e = getenv("PT_WF_FUSED");
+    return !(e && e[0] == '0');
+}
+
+static uint32_t trace_slice() {
+    static const uint32_t s = [] {
+        const char *e = getenv("PT_WF_TRACE_SLICE");  // tuning knob: ids per run dealt to a block
+        const long v = e ? atol(e) : 256;
+        return (uint32_t)(v < 1 ? 1 : (v > (1l << 20) ? (1l << 20) : v));
+    }();
+    return s;
+}
+
+template <bool FIRST>
+static void launch_trace(hipStream_t st, const dev::Scene &sc, const FrameParams &P, const WfView &v, int it,
+                         int fkind) {
+    const uint32_t slice = trace_slice();
+    if (sc.ext) {
+        static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY, true>);
+        wf_trace<FIRST, 2, march::F_ANY, true><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+    } else if (fkind != march::F_HEART) {
+        static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY>);
+        wf_trace<FIRST, 2, march::F_ANY><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+    } else {
+        static const uint32_t nb = resident_blocks(wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART>);
+        wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+    }
+}
+
 // Chunks in flight: each has its own path state (slot) and runs on its own
 // stream, so one chunk's bounce/compaction kernels fill the tails of the
 // other's march kernels (and its memory-bound bounces overlap the other's
@@ -781,6 +942,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         for (int k = 0; k < slots - 1; k++)
             if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
     }
+    const bool fused = fused_bounces() && !ws->diag;
     uint64_t c = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
@@ -802,13 +964,15 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
             if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-            launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind);
+            if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind);
+            else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
                     if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-                    launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind);
+                    if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind);
+                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 }

@@ -1,0 +1,72 @@
+"""Per-rank render time of the N-GPU tile partition, simulated on one GPU.
+
+For world N, each rank r renders its round-robin tiles (render_device with
+rank r of N) into its compact shard; the N-GPU frame time is the slowest
+rank's (plus the gather).  Running every rank's share on the one GPU we have
+gives that time without the other GPUs:
+
+    python scripts/rank_sim.py [--worlds 1,8] [--spp 256] [--reps 2]
+
+Prints one JSON line per world: max/mean rank ms and the projected strong
+scaling efficiency t1 / (N * max_rank_ms) (the driver measures the real one).
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--ranks", default="", help="subset of ranks to time (default: all)")
+    a = ap.parse_args()
+    import torch
+    import __graft_entry__ as ge
+    pt = ge.load_package()
+    text = (ROOT / "scenes" / "cornell_box.json").read_text()
+    scene = pt.Scene.from_json(text, seed=1)
+    r = pt.HipRenderer(scene, device=0, depth=8)
+    cam = scene.camera()
+    W, H, spp = a.width, a.height, a.spp
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    buf = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
+    t1 = None
+    for world in [int(x) for x in a.worlds.split(",")]:
+        ranks = [int(x) for x in a.ranks.split(",")] if a.ranks else list(range(world))
+        ms = []
+        for rank in ranks:
+            if rank >= world:
+                continue
+            r.render_device(cam, W, H, spp, 1, rank, world, buf.data_ptr(), sp)  # warm
+            torch.cuda.synchronize()
+            best = 1e30
+            for _ in range(a.reps):
+                t = time.perf_counter()
+                r.render_device(cam, W, H, spp, 1, rank, world, buf.data_ptr(), sp)
+                torch.cuda.synchronize()
+                best = min(best, (time.perf_counter() - t) * 1e3)
+            ms.append(best)
+            print("world %d rank %d: %.1f ms" % (world, rank, best), file=sys.stderr, flush=True)
+        mx = max(ms)
+        if world == 1:
+            t1 = mx
+        rec = {"world": world, "max_rank_ms": round(mx, 2), "mean_rank_ms": round(sum(ms) / len(ms), 2),
+               "msamples_s": round(W * H * spp / mx / 1e3, 1)}
+        if t1:
+            rec["projected_eff"] = round(t1 / (world * mx), 3)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -223,6 +223,27 @@ def test_engines_agree_with_oracle(pt, cornell):
     check_image(wave, osc.render(80, 45, 3, 8, 21))
 
 
+def test_fused_bounces_equal_per_bounce_launches(pt, cornell, spheres):
+    """wf_trace (paths run bounce after bounce in registers until a march or
+    their end) against one wf_bounce launch per bounce: the same bits, on the
+    Heart build (cornell), the generic build at GUI depth (spheres) and with
+    tiny chunks and tile groups."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam, ip = ps.camera(), pt.ImageParams(96, 54)
+    with _env(PT_ENGINE="wave"):
+        fused = r.render(cam, ip, 4, seed=31)
+        with _env(PT_WF_FUSED=0):
+            split = r.render(cam, ip, 4, seed=31)
+        assert np.array_equal(fused, split)
+        with _env(PT_WF_PATHS=256 * 3):
+            small = r.render(cam, ip, 4, seed=31)
+        assert np.array_equal(fused, small)
+        img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
+        check_image(img, ref)
+    check_image(fused, osc.render(96, 54, 4, 8, 31))
+
+
 def test_wavefront_chunks_and_tile_groups(pt, cornell):
     """A tiny path budget forces one-tile groups and one-sample chunks: the
     running per-pixel sums must still add samples in order."""

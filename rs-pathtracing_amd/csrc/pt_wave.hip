@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         for (int k = 0; k < 4; k++) atomicAdd(&diag[36 + k], dsec[k]);
 }
 
-// Fused bounces (the default engine step): a lane carries its path through as
+// Fused bounces (PT_WF_FUSED=1; measured slower, see fused_bounces()): a lane carries its path through as
 // many bounces as it can without a march — shade the pending hit, trace the
 // new ray, and if no marched shape's bound starts before the best hit, shade
 // that hit at once in registers and go on.  Path state goes to HBM only when
@@ -777,12 +777,15 @@ static uint32_t resident_blocks(K kern) {
     return (uint32_t)(cus * occ);
 }
 
-// The fused bounce step (wf_trace) unless PT_WF_FUSED=0 in the environment
-// (read per render: one wf_bounce launch per bounce, the engine before fusion,
-// kept for A/B tests; the diag build always runs wf_bounce).
+// The fused bounce step (wf_trace) only with PT_WF_FUSED=1 in the environment
+// (read per render).  Measured on C2: 1119 M samples/s fused against 1176 with
+// one wf_bounce launch per bounce — the bounce is VALU-bound, not bound by the
+// path-state traffic fusion removes, and the per-bounce launches interleave
+// better with the other chunk's marches — so per-bounce launches are the
+// default.  The diag build always runs wf_bounce.
 static bool fused_bounces() {
     const char *e = getenv("PT_WF_FUSED");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 static uint32_t trace_slice() {
@@ -845,6 +848,14 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     return hipSuccess;
 }
 
+// Minimum sample chunks per frame (PT_WF_MIN_CHUNKS, read per render).
+constexpr uint32_t MIN_CHUNK_PATHS = 1u << 21;
+static uint32_t min_chunks() {
+    const char *e = getenv("PT_WF_MIN_CHUNKS");
+    const long v = e ? atol(e) : 1;
+    return (uint32_t)(v < 1 ? 1 : (v > 4096 ? 4096 : v));
+}
+
 struct Slot {
     WfView v;
     uint32_t *cp_blk;
@@ -862,6 +873,19 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     uint32_t ns = cap_want / npix_max;
     if (ns < 1) ns = 1;
     if (ns > P0.spp) ns = P0.spp;
+    {
+        // A small frame (one rank's share of a multi-GPU frame) still gets at
+        // least min_chunks() sample chunks, so the pipelined slots overlap one
+        // chunk's short tail iterations with the next chunk's work; chunks
+        // keep at least MIN_CHUNK_PATHS paths to fill the device.
+        const uint32_t mc = min_chunks();
+        if (mc > 1 && ntiles <= group_tiles) {
+            uint32_t want = (P0.spp + mc - 1) / mc;
+            const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;
+            if (want < floor_ns) want = floor_ns;
+            if (want < ns) ns = want;
+        }
+    }
     const uint32_t cap = ns * npix_max;
     const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
     const size_t cnt_words = (size_t)(iters + 2) * 4;

@@ -232,15 +232,15 @@ def test_fused_bounces_equal_per_bounce_launches(pt, cornell, spheres):
     r = pt.HipRenderer(ps, depth=8)
     cam, ip = ps.camera(), pt.ImageParams(96, 54)
     with _env(PT_ENGINE="wave"):
-        fused = r.render(cam, ip, 4, seed=31)
-        with _env(PT_WF_FUSED=0):
-            split = r.render(cam, ip, 4, seed=31)
-        assert np.array_equal(fused, split)
-        with _env(PT_WF_PATHS=256 * 3):
-            small = r.render(cam, ip, 4, seed=31)
-        assert np.array_equal(fused, small)
-        img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
-        check_image(img, ref)
+        split = r.render(cam, ip, 4, seed=31)
+        with _env(PT_WF_FUSED=1):
+            fused = r.render(cam, ip, 4, seed=31)
+            assert np.array_equal(fused, split)
+            with _env(PT_WF_PATHS=256 * 3):
+                small = r.render(cam, ip, 4, seed=31)
+            assert np.array_equal(fused, small)
+            img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
+            check_image(img, ref)
     check_image(fused, osc.render(96, 54, 4, 8, 31))
 
 

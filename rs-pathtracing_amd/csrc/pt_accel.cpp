@@ -72,10 +72,30 @@ struct Builder {
     const std::vector<DBox> &boxes;
     Accel &out;
     static constexpr int LEAF = 2;
+    // the tree in build order: node box (DNode with first/count for leaves),
+    // split axis and children (-1 for a leaf)
+    struct TNode {
+        DNode n;
+        int axis, left, right;
+    };
+    std::vector<TNode> tree;
 
-    void emit(std::vector<int32_t> &ids, size_t a, size_t b) {
-        size_t me = out.nodes.size();
-        out.nodes.push_back(DNode{});
+    // one threaded layout: DFS with the near child first for the octant's
+    // direction signs; skip = index after the subtree, relative to `base`
+    void thread(int t, int oct, size_t base) {
+        const size_t me = out.nodes.size();
+        out.nodes.push_back(tree[t].n);
+        if (tree[t].left >= 0) {
+            const bool neg = (oct >> tree[t].axis) & 1;  // moving toward -axis: the high half is nearer
+            thread(neg ? tree[t].right : tree[t].left, oct, base);
+            thread(neg ? tree[t].left : tree[t].right, oct, base);
+        }
+        out.nodes[me].skip = (int32_t)(out.nodes.size() - base);
+    }
+
+    int emit(std::vector<int32_t> &ids, size_t a, size_t b) {
+        const int me = (int)tree.size();
+        tree.push_back(TNode{DNode{}, 0, -1, -1});
         DNode n{};
         for (int k = 0; k < 3; k++) {
             n.lo[k] = INFINITY;
@@ -96,9 +116,8 @@ struct Builder {
             n.first = (int32_t)out.leaf.size();
             n.count = (int32_t)(b - a);
             for (size_t i = a; i < b; i++) out.leaf.push_back(ids[i]);
-            n.skip = (int32_t)out.nodes.size();
-            out.nodes[me] = n;
-            return;
+            tree[me].n = n;
+            return me;
         }
         int axis = 0;
         for (int k = 1; k < 3; k++)
@@ -108,12 +127,12 @@ struct Builder {
             double cx = boxes[x].lo[axis] + boxes[x].hi[axis], cy = boxes[y].lo[axis] + boxes[y].hi[axis];
             return cx < cy || (cx == cy && x < y);
         });
-        emit(ids, a, mid);
-        emit(ids, mid, b);
+        const int l = emit(ids, a, mid);
+        const int r = emit(ids, mid, b);
         n.count = 0;
         n.first = 0;
-        n.skip = (int32_t)out.nodes.size();
-        out.nodes[me] = n;
+        tree[me] = TNode{n, axis, l, r};
+        return me;
     }
 };
 
@@ -134,8 +153,10 @@ Accel build_accel(const Scene &sc, int json_shapes) {
         else rest.push_back(i);
     }
     if (!rest.empty()) {
-        Builder b{a.boxes, a};
-        b.emit(rest, 0, rest.size());
+        Builder b{a.boxes, a, {}};
+        const int root = b.emit(rest, 0, rest.size());
+        a.nodes.reserve(b.tree.size() * BVH_OCTANTS);
+        for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());
     }
     return a;
 }

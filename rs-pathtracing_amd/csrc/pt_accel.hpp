@@ -21,8 +21,17 @@
 
 namespace pt {
 
+// The BVH is stored as 8 threaded (stackless, skip-pointer) layouts of the same
+// tree, one per ray-direction octant: layout o = (d.x < 0) | (d.y < 0) << 1 |
+// (d.z < 0) << 2 visits, at every interior node, the child on the ray's near
+// side of the split first, so the best hit shrinks early and far subtrees are
+// skipped by their boxes.  Skip indices are relative to the layout; the leaf
+// id ranges are shared.  8x the node memory (C5: ~50 MB of the 288 GB HBM)
+// buys front-to-back order without a per-lane stack.
+constexpr int BVH_OCTANTS = 8;
 struct Accel {
-    std::vector<DNode> nodes;
+    std::vector<DNode> nodes;    // BVH_OCTANTS layouts of nodes_per_octant() nodes each
+    int nodes_per_octant() const { return (int)(nodes.size() / BVH_OCTANTS); }
     std::vector<int32_t> leaf;   // shape ids referenced by leaf nodes
     std::vector<int32_t> lin;    // wave-uniform list
     std::vector<int32_t> march;  // ray-marched shapes

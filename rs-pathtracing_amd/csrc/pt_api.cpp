@@ -224,7 +224,7 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     }
     r->ds.nshapes = (int)hs.size();
     r->ds.nmats = (int)hm.size();
-    r->ds.nnodes = (int)acc.nodes.size();
+    r->ds.nnodes = acc.nodes_per_octant();  // nodes per octant layout
     r->ds.nlin = (int)acc.lin.size();
     r->ds.nmarch = (int)acc.march.size();
     r->ds.ext = S.textures.empty() ? 0 : 1;

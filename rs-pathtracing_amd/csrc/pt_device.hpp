@@ -295,10 +295,13 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
             who = i;
         }
     }
-    // threaded BVH over the remaining non-marched shapes
+    // threaded BVH over the remaining non-marched shapes, in the layout of the
+    // ray's direction octant (near child first, pt_accel.hpp)
+    const DNode *nodes = sc.nodes + (size_t)((r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0)) *
+                                        (size_t)sc.nnodes;
     int n = 0;
     while (n < sc.nnodes) {
-        const DNode &nd = sc.nodes[n];
+        const DNode &nd = nodes[n];
         if (STATS) ct->c[C_NODE_SLABS]++;
         if (slab(nd.lo, nd.hi, r, inv, min_t, best)) {
             for (int k = 0; k < nd.count; k++) {

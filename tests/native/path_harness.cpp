@@ -40,7 +40,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.perlin = tex ? b->sc.perlins.data() : nullptr;
         b->view.images = tex ? b->sc.images.data() : nullptr;
         b->view.pixels = tex ? b->sc.pixels.data() : nullptr;
-        b->view.nnodes = (int)b->acc.nodes.size();
+        b->view.nnodes = b->acc.nodes_per_octant();
         b->view.nlin = (int)b->acc.lin.size();
         b->view.nmarch = (int)b->acc.march.size();
         b->view.diag = 0;
@@ -53,7 +53,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
 extern "C" void h_scene_free(void *p) { delete (Bundle *)p; }
 extern "C" void h_accel_stats(void *p, int *out) {
     Bundle *b = (Bundle *)p;
-    out[0] = (int)b->acc.nodes.size();
+    out[0] = b->acc.nodes_per_octant();
     out[1] = (int)b->acc.lin.size();
     out[2] = (int)b->acc.march.size();
     out[3] = (int)b->acc.leaf.size();

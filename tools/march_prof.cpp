@@ -119,7 +119,7 @@ int main(int argc, char **argv) {
         v.lin = acc.lin.data();
         v.march = acc.march.data();
         v.boxes = acc.boxes.data();
-        v.nnodes = (int)acc.nodes.size();
+        v.nnodes = acc.nodes_per_octant();
         v.nlin = (int)acc.lin.size();
         v.nmarch = (int)acc.march.size();
         const uint32_t W = 1920, H = 1080;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace pt {
 
@@ -71,7 +72,7 @@ namespace {
 struct Builder {
     const std::vector<DBox> &boxes;
     Accel &out;
-    static constexpr int LEAF = 2;
+    int leaf_max = 2;  // shapes per leaf (PT_BVH_LEAF, tuning knob)
     // the tree in build order: node box (DNode with first/count for leaves),
     // split axis and children (-1 for a leaf)
     struct TNode {
@@ -112,7 +113,7 @@ struct Builder {
                 chi[k] = std::max(chi[k], c);
             }
         }
-        if (b - a <= (size_t)LEAF) {
+        if (b - a <= (size_t)leaf_max) {
             n.first = (int32_t)out.leaf.size();
             n.count = (int32_t)(b - a);
             for (size_t i = a; i < b; i++) out.leaf.push_back(ids[i]);
@@ -152,8 +153,31 @@ Accel build_accel(const Scene &sc, int json_shapes) {
         else if ((small && i < json_shapes) || sc.shapes[i].type == TORUS) a.lin.push_back(i);
         else rest.push_back(i);
     }
+    // A shape whose box dwarfs the typical one (a ground sphere under a field
+    // of small ones) would inflate the box of every ancestor of its leaf, so
+    // rays would enter those nodes everywhere: it joins the wave-uniform list
+    // instead (while that list has room).
+    if (rest.size() > 64) {
+        auto ext = [&](int32_t i) {
+            const DBox &b = a.boxes[i];
+            return std::max({b.hi[0] - b.lo[0], b.hi[1] - b.lo[1], b.hi[2] - b.lo[2]});
+        };
+        std::vector<double> e;
+        e.reserve(rest.size());
+        for (int32_t i : rest) e.push_back(ext(i));
+        std::nth_element(e.begin(), e.begin() + e.size() / 2, e.end());
+        const double big = 64.0 * e[e.size() / 2];
+        std::vector<int32_t> keep;
+        keep.reserve(rest.size());
+        for (int32_t i : rest) {
+            if (ext(i) > big && a.lin.size() < (size_t)LIN_MAX) a.lin.push_back(i);
+            else keep.push_back(i);
+        }
+        rest.swap(keep);
+    }
     if (!rest.empty()) {
-        Builder b{a.boxes, a, {}};
+        Builder b{a.boxes, a};
+        if (const char *e = getenv("PT_BVH_LEAF")) b.leaf_max = std::max(1, std::min(16, atoi(e)));
         const int root = b.emit(rest, 0, rest.size());
         a.nodes.reserve(b.tree.size() * BVH_OCTANTS);
         for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());

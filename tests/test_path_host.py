@@ -143,3 +143,37 @@ def test_many_json_shapes_go_to_bvh(H):
         who, t, *_ = pr.closest(np.concatenate([o, d]))
         h = pr.o.closest_hit(o, d)
         assert (who, t if who >= 0 else None) == ((h.shape, h.t) if h else (-1, None))
+
+
+def test_synthetic_field_ground_sphere_uniform_and_octant_bvh(H):
+    """C5's recipe at 3,000 spheres: the radius-1000 ground sphere leaves the
+    BVH for the wave-uniform list (its box would inflate every ancestor), the
+    rest sit in the 8 octant-ordered layouts; closest hits and pixel samples
+    equal the oracle's linear scan bit for bit."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    text = json.dumps(make_scenes.synthetic(3000))
+    pr = Pair(H, text, seed=1)
+    st = (C.c_int * 4)()
+    H.h_accel_stats(pr.h, st)
+    nodes, nlin, nmarch, nleaf = list(st)
+    assert nlin == 1 and nmarch == 0 and nleaf == pr.o.num_shapes - 1
+    rng = np.random.default_rng(5)
+    for _ in range(1500):
+        o = rng.uniform([-15, 0.05, -15], [15, 3, 15])
+        d = rng.normal(size=3)
+        d[1] = -abs(d[1]) if rng.random() < 0.7 else d[1]
+        d /= np.linalg.norm(d)
+        who, t, p, n, f = pr.closest(np.concatenate([o, d]))
+        h = pr.o.closest_hit(o, d)
+        if h is None:
+            assert who == -1
+        else:
+            assert (who, t, p, n, f) == (h.shape, h.t, list(h.point), list(h.normal), h.front_face)
+    w, h = 320, 180
+    px = rng.choice(w * h, size=60, replace=False).astype(np.uint32)
+    out = np.zeros((len(px), 3))
+    H.h_trace_pixels(pr.h, w, h, 2, 8, 3, px.ctypes.data_as(C.POINTER(C.c_uint32)), len(px),
+                     out.ctypes.data_as(C.POINTER(C.c_double)))
+    assert np.array_equal(out, pr.o.render(w, h, 2, 8, 3, pixels=px))

@@ -158,6 +158,9 @@ struct Ray {
 #ifndef PT_LAZY_RECT
 #define PT_LAZY_RECT 1
 #endif
+#ifndef PT_LIN_BOX
+#define PT_LIN_BOX 1  // padded-box pre-test for cubes and spheres on the wave-uniform list
+#endif
 // MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
 // every one on the march list), so the march branch is not compiled in.
 // EXT: the extended build (scenes with a Torus or non-solid textures) that
@@ -289,6 +292,14 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     for (int k = 0; k < sc.nlin; k++) {
         const int i = uniform_load(&sc.lin[k]);
         const DShape s = uniform_shape(&sc.shapes[i]);
+        if (PT_LIN_BOX && (s.type == CUBE || s.type == SPHERE)) {
+            // the padded world box first (12 FLOP with the caller's 1/d):
+            // a miss there is a miss of the exact test, which costs a full
+            // inverse transform and, for a cube, six divisions
+            if (STATS) ct->c[C_NODE_SLABS]++;
+            const DBox b = uniform_box(&sc.boxes[i]);
+            if (!slab(b.lo, b.hi, r, inv, min_t, best)) continue;
+        }
         double t;
         if (shape_test<STATS, march::F_ANY, false, EXT>(s, r, min_t, best, &t, ct) && (t < best || i > who)) {
             best = t;

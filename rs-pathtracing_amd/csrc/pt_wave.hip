@@ -94,6 +94,36 @@ struct MemStack {
     }
 };
 
+// dev::unwind for an HBM id stack, with the loads batched: the top UB ids are
+// loaded together, then their albedos together, then multiplied in the
+// recursion's order (top of the stack first, as dev::unwind pops them), so a
+// path of n bounces waits for 2*ceil(n/UB) dependent round trips instead of
+// 2n.  Textured (EXT) stacks take the generic unwind.
+constexpr int UB = 4;
+template <bool EXT>
+__device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3 c) {
+    if (EXT) return dev::unwind<false, true>(sc, stk, c);
+    while (stk.n > 0) {
+        const int m = stk.n < UB ? stk.n : UB;
+        uint32_t id[UB];
+#pragma unroll
+        for (int j = 0; j < UB; j++) id[j] = j < m ? stk.base[(size_t)(stk.n - 1 - j) * stk.stride] : 0u;
+        double ax[UB], ay[UB], az[UB];
+#pragma unroll
+        for (int j = 0; j < UB; j++) {
+            const DMaterial &mt = sc.mats[id[j]];
+            ax[j] = j < m ? mt.albedo[0] : 1.0;
+            ay[j] = j < m ? mt.albedo[1] : 1.0;
+            az[j] = j < m ? mt.albedo[2] : 1.0;
+        }
+#pragma unroll
+        for (int j = 0; j < UB; j++)
+            if (j < m) c = dev::v3(ax[j] * c.x, ay[j] * c.y, az[j] * c.z);  // Vector3d::product
+        stk.n -= m;
+    }
+    return c;
+}
+
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
 // thread-in-tile laid out as render_tiles' 4 waves of 8x8.
 __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v, uint32_t id, uint32_t *x,
@@ -163,7 +193,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 if (EXT) stk.vb = v.att + id;
                 V3 leaf;
                 if (dev::shade<false, FK, EXT>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
-                    const V3 c = dev::unwind<false, EXT>(sc, stk, leaf);
+                    const V3 c = unwind_mem<EXT>(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
                     v.rz[id] = c.z;
@@ -280,7 +310,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
         if (!done && shade_now) {
             V3 leaf;
             if (dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf)) {
-                const V3 c = dev::unwind<false, EXT>(sc, stk, leaf);
+                const V3 c = unwind_mem<EXT>(sc, stk, leaf);
                 v.rx[id] = c.x;
                 v.ry[id] = c.y;
                 v.rz[id] = c.z;

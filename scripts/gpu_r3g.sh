@@ -1,0 +1,9 @@
+# Batched HBM unwind: GPU suite, C2 twice, bounce section diag
+set -e
+OUT=$GRAFT_REPO_ROOT/gpurun_out/r3g
+mkdir -p $OUT
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $OUT/bench_c2_a.json 2> $OUT/bench_c2_a.err
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-parity > $OUT/bench_c2_b.json 2> $OUT/bench_c2_b.err
+timeout -k 10 200 python -u scripts/wave_diag.py 8 > $OUT/wave_diag.txt 2>&1

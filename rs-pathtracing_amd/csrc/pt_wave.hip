@@ -634,104 +634,6 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     }
 }
 
-// Marches of iteration `it`, dealt to waves from one global cursor (the
-// default; PT_WF_MARCH_DEAL=block selects wf_march's per-block shares).  Each
-// wave owns a run of `run` consecutive queue positions at a time (pixel-
-// coherent jobs) and hands them to its lanes that have no job; when the run
-// cannot serve them all, one lane takes the next run with a single global
-// atomic on cnt[it * 4 + 2] (zeroed with the chunk's counters).  No lane of
-// any wave idles while unclaimed jobs remain anywhere in the queue: the
-// per-block shares left a wave's lanes idle once the block's share was
-// drained while a few long marches kept the wave alive.  Each job runs the
-// same select/march code as wf_march, so (best, who) are the same bits.
-template <int FK = march::F_ANY>
-__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march_w(dev::Scene sc, WfView v, int it, uint32_t run) {
-    const int nm = sc.nmarch;
-    const uint32_t count = v.cnt[it * 4 + 1];
-    uint32_t *cursor = &v.cnt[it * 4 + 2];
-    const uint32_t *mq = v.mq;
-    const uint32_t lane = lane_id();
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
-    uint32_t wnext = 0, wend = 0;  // the wave's current run [wnext, wend) (wave-uniform)
-    bool have = false, marching = false;
-    MarchJob cur;
-    cur.id = 0;
-    cur.ray.o = cur.ray.d = dev::v3(0.0, 0.0, 0.0);
-    cur.best = 0.0;
-    cur.who = -1;
-    int km = 0, mshape = -1;
-    V3 inv = dev::v3(0.0, 0.0, 0.0);
-    march::MarchState ms;
-    march::MarchStats mst{0, 0, 0};
-    for (;;) {
-        // deal queue positions to the lanes without a job
-        const uint64_t need = __ballot(!have);
-        if (need) {
-            const uint32_t n = (uint32_t)__popcll(need);
-            const uint32_t avail = wend - wnext;
-            uint32_t nb = 0;
-            if (n > avail) {  // wave-uniform: take the next run
-                const uint32_t leader = (uint32_t)__ffsll((unsigned long long)__ballot(true)) - 1u;
-                uint32_t b = 0;
-                if (lane == leader) b = atomicAdd(cursor, run);
-                nb = (uint32_t)__shfl((int)b, (int)leader, 64);
-            }
-            if (!have) {
-                const uint32_t rank = (uint32_t)__popcll(need & lt);
-                const uint32_t p = rank < avail ? wnext + rank : nb + (rank - avail);
-                if (p < count) {
-                    have = true;
-                    load_job(v, mq[p], &cur);
-                    inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
-                    km = 0;
-                    marching = false;
-                }
-            }
-            if (n > avail) {
-                wnext = nb + (n - avail);
-                wend = nb + run;
-            } else {
-                wnext += n;
-            }
-        }
-        if (__ballot(have) == 0) break;  // the queue is drained and every lane is done
-        if (!have) continue;
-        bool done = false;
-        if (marching) {
-            const int st = march::march_iter<false, true, FK>(ms, &mst);
-            if (st != march::M_RUNNING) {
-                // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
-                if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) && (ms.t < cur.best || mshape > cur.who)) {
-                    cur.best = ms.t;
-                    cur.who = mshape;
-                }
-                marching = false;
-            }
-        } else {
-            // select: next marched shape whose bound is entered before `best`
-            while (km < nm) {
-                const int s = sc.march[km++];
-                const DBox &b = sc.boxes[s];
-                if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;
-                const DShape &S = sc.shapes[s];
-                const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                if (march::march_begin<FK>(dev::shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z,
-                                           &ms)) {
-                    mshape = s;
-                    marching = true;
-                    break;
-                }
-            }
-            done = !marching;
-        }
-        if (done) {
-            v.t[cur.id] = cur.best;
-            v.who[cur.id] = cur.who;
-            have = false;
-        }
-    }
-}
-
 // In-order per-pixel sum of the chunk's samples; mean after the last chunk.
 __global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int first, int last,
                                                  double *__restrict__ out) {
@@ -1095,11 +997,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
     }
     const bool fused = fused_bounces() && !ws->diag;
-    // march dealing: waves from one global cursor (wf_march_w) unless
-    // PT_WF_MARCH_DEAL=block (wf_march's per-block shares; read per render)
-    const char *deal_env = getenv("PT_WF_MARCH_DEAL");
-    const bool wave_deal = !(deal_env && deal_env[0] == 'b');
-    const uint32_t march_run = march_slice < 64 ? 64u : march_slice;  // a run must cover a wave's 64 lanes
     uint64_t c = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
@@ -1143,15 +1040,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
-                if (wave_deal && !ws->diag) {
-                    if (fkind != march::F_HEART) {
-                        static const uint32_t nb = resident_blocks(wf_march_w<march::F_ANY>);
-                        wf_march_w<march::F_ANY><<<nb, 256, 0, cs>>>(sc, v, it, march_run);
-                    } else {
-                        static const uint32_t nb = resident_blocks(wf_march_w<march::F_HEART>);
-                        wf_march_w<march::F_HEART><<<nb, 256, 0, cs>>>(sc, v, it, march_run);
-                    }
-                } else if (fkind != march::F_HEART)
+                if (fkind != march::F_HEART)
                     wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
                 else if (ws->diag)
                     wf_march<true, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, ws->diag, march_slice);

@@ -229,12 +229,13 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         const double *m = s.inv;
         const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
-        const double tt = -oz / dz;
-        if (tt < min_t || tt > max_t) return false;
         const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
         const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
         const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
         const double dy = r.d.x * m[4] + r.d.y * m[5] + r.d.z * m[6];
+        if (PT_QUICK_REJECT && rect_quick_miss(s.p, ox, oy, oz, dx, dy, dz, min_t, max_t)) return false;
+        const double tt = -oz / dz;
+        if (tt < min_t || tt > max_t) return false;
         const double px = ox + dx * tt, py = oy + dy * tt;
         if (px < s.p[0] || px > s.p[2] || py < s.p[1] || py > s.p[3]) return false;
         *t = tt;

@@ -116,62 +116,8 @@ PT_HD bool rect_t(const double *p, V3 o, V3 d, double min_t, double max_t, doubl
     *t = tt;
     return true;
 }
-// Quick rejections without the correctly rounded divisions (PT_QUICK_REJECT).
-// A quotient n / d is estimated as n * r, r = march::approx_rcp(d) (hardware
-// reciprocal + two Newton steps: a few ulp), so every estimate is within
-// 1e-14 relative of the exact quotient the reference computes.  A test is
-// rejected only when its estimate misses by more than 1e-12 relative — then
-// the exact quotient misses too; everything closer, and every non-finite
-// input (zero direction components, NaN, inf, with the reference's NaN
-// quirks), takes the exact path unchanged.  Exact rejections cost ~10 VALU
-// instructions per division; these cost ~4.
-#ifndef PT_QUICK_REJECT
-#define PT_QUICK_REJECT 1
-#endif
-constexpr double QR_REL = 1e-12;
-PT_HD bool qr_finite(double x) { return fabs(x) < 1e300; }  // false for inf and NaN
-// a divisor the estimate handles: finite and far from the subnormal range
-PT_HD bool qr_divisor(double d) { return fabs(d) > 1e-290 && fabs(d) < 1e290; }
-
-// Cube: the six slab quotients estimated; a definite miss of the slab test
-// (tmin > tmax or tmin > max_t, with the estimates' error bound on both) is a
-// miss of the exact test.
-PT_HD bool cube_quick_miss(V3 o, V3 d, double min_t, double max_t) {
-    if (!(qr_finite(o.x) && qr_finite(o.y) && qr_finite(o.z) && qr_divisor(d.x) && qr_divisor(d.y) &&
-          qr_divisor(d.z)))
-        return false;
-    const double rx = march::approx_rcp(d.x), ry = march::approx_rcp(d.y), rz = march::approx_rcp(d.z);
-    const double lx = (-1.0 - o.x) * rx, ly = (-1.0 - o.y) * ry, lz = (-1.0 - o.z) * rz;
-    const double ux = (1.0 - o.x) * rx, uy = (1.0 - o.y) * ry, uz = (1.0 - o.z) * rz;
-    const double m = fmax(fmax(fmax(fabs(lx), fabs(ux)), fmax(fabs(ly), fabs(uy))), fmax(fabs(lz), fabs(uz)));
-    if (!qr_finite(m)) return false;
-    const double e = QR_REL * (m + fabs(min_t));  // bounds |estimate - exact| of tmin and tmax
-    const double tmin = fmax(fmax(fmax(fmin(lx, ux), fmin(ly, uy)), fmin(lz, uz)), min_t);
-    const double tmax = fmin(fmin(fmin(fmax(lx, ux), fmax(ly, uy)), fmax(lz, uz)), max_t);
-    return tmin - tmax > 2.0 * e || tmin - max_t > e;
-}
-
-// Rectangle: tt = -o.z / d.z estimated; a plane crossing clearly outside
-// [min_t, max_t], or a crossing point clearly outside the rectangle, is a
-// miss of the exact test.
-PT_HD bool rect_quick_miss(const double *p, double ox, double oy, double oz, double dx, double dy, double dz,
-                           double min_t, double max_t) {
-    if (!(qr_divisor(dz) && qr_finite(oz))) return false;
-    const double tt = -oz * march::approx_rcp(dz);
-    if (!qr_finite(tt)) return false;
-    const double et = QR_REL * (fabs(tt) + fabs(min_t));
-    if (min_t - tt > et) return true;
-    if (tt - max_t > QR_REL * (fabs(tt) + fabs(max_t))) return true;  // never for max_t = inf
-    if (!(qr_finite(ox) && qr_finite(oy) && qr_finite(dx) && qr_finite(dy))) return false;
-    const double px = ox + dx * tt, py = oy + dy * tt;
-    const double ex = QR_REL * (fabs(ox) + fabs(dx * tt) + fabs(p[0]) + fabs(p[2]));
-    const double ey = QR_REL * (fabs(oy) + fabs(dy * tt) + fabs(p[1]) + fabs(p[3]));
-    return p[0] - px > ex || px - p[2] > ex || p[1] - py > ey || py - p[3] > ey;
-}
-
 // Cube::ray_intersect (shapes/mod.rs:250-285), slab on [-1, 1]^3
 PT_HD bool cube_t(V3 o, V3 d, double min_t, double max_t, double *t) {
-    if (PT_QUICK_REJECT && cube_quick_miss(o, d, min_t, max_t)) return false;
     double lx = (-1.0 - o.x) / d.x, ly = (-1.0 - o.y) / d.y, lz = (-1.0 - o.z) / d.z;
     double ux = (1.0 - o.x) / d.x, uy = (1.0 - o.y) / d.y, uz = (1.0 - o.z) / d.z;
     double tmin = fmax(fmax(fmax(fmin(lx, ux), fmin(ly, uy)), fmin(lz, uz)), min_t);
@@ -229,13 +175,12 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         const double *m = s.inv;
         const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
+        const double tt = -oz / dz;
+        if (tt < min_t || tt > max_t) return false;
         const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
         const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
         const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
         const double dy = r.d.x * m[4] + r.d.y * m[5] + r.d.z * m[6];
-        if (PT_QUICK_REJECT && rect_quick_miss(s.p, ox, oy, oz, dx, dy, dz, min_t, max_t)) return false;
-        const double tt = -oz / dz;
-        if (tt < min_t || tt > max_t) return false;
         const double px = ox + dx * tt, py = oy + dy * tt;
         if (px < s.p[0] || px > s.p[2] || py < s.p[1] || py > s.p[3]) return false;
         *t = tt;

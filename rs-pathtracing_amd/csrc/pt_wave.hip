@@ -470,9 +470,6 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_UNITS
 #define PT_WF_UNITS 1
 #endif
-#ifndef PT_WF_SEL_SCALAR
-#define PT_WF_SEL_SCALAR 1  // select with scalar loads when the scene has one marched shape
-#endif
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 5  // waves per SIMD the march kernel's registers must allow
 #endif
@@ -595,25 +592,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 }
             } else {
                 // select: next marched shape whose bound is entered before `best`
-                if (PT_WF_SEL_SCALAR && nm == 1) {
-                    // one marched shape (cornell's Heart): its box and transform
-                    // are wave-uniform, read with scalar loads (the scalar
-                    // cache) instead of per-lane gathers from L2
-                    if (km == 0) {
-                        km = 1;
-                        const int s = dev::uniform_load(&sc.march[0]);
-                        const DBox b = dev::uniform_box(&sc.boxes[s]);
-                        if (dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) {
-                            const DShape S = dev::uniform_shape(&sc.shapes[s]);
-                            const V3 o = dev::xf_point(S.inv, cur.ray.o), d = dev::xf_vector(S.inv, cur.ray.d);
-                            if (march::march_begin<FK>(dev::shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x,
-                                                       d.y, d.z, &ms)) {
-                                mshape = s;
-                                marching = true;
-                            }
-                        }
-                    }
-                } else while (km < nm) {
+                while (km < nm) {
                     const int s = sc.march[km++];
                     const DBox &b = sc.boxes[s];
                     if (!dev::slab(b.lo, b.hi, cur.ray, inv, T_MIN, cur.best)) continue;

@@ -471,7 +471,7 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #define PT_WF_UNITS 1
 #endif
 #ifndef PT_WF_MARCH_WAVES
-#define PT_WF_MARCH_WAVES 5  // waves per SIMD the march kernel's registers must allow
+#define PT_WF_MARCH_WAVES 4  // waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs, 20 B: 1273; 3: 1261)
 #endif
 struct MarchJob {
     uint32_t id;

@@ -248,6 +248,16 @@ def main():
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
         }
+        # roofline.traffic: HBM bytes per launch of the same kernel from the committed PMC passes of this
+        # workload (scripts/pmc_traffic.py; bench.py cannot read PMC counters itself)
+        tfile = ROOT / "profiles" / "r1" / "pmc_traffic_c2.json"
+        if tfile.exists():
+            tr = json.loads(tfile.read_text())
+            kind = tr.get("kinds", {}).get(dom)
+            if tr.get("workload") == rec["config"]["workload"] and kind and world == 1:
+                rec["roofline"]["traffic"] = round(kind["traffic"])
+                rec["roofline"]["traffic_source"] = "profiles/r1/pmc_traffic_c2.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+                rec["roofline"]["traffic_gbs"] = round(kind["traffic"] / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
         if not args.no_parity:
             import oracle
             rng = np.random.default_rng(1234)

@@ -1,7 +1,7 @@
 # Round-1 evidence run on one MI355X: GPU tests, smoke, default bench, rocprofv3
 # kernel stats of the same bench command, PMC FETCH/WRITE passes (separate runs).
 set -e
-OUT=$GRAFT_REPO_ROOT/gpurun_out/r1final
+OUT=$GRAFT_REPO_ROOT/gpurun_out/r1final_mw4
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 timeout -k 10 400 python -m pytest tests -q -x -m gpu > $OUT/pytest_gpu.log 2>&1

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <stdexcept>
 
 namespace pt {
 
@@ -181,6 +182,22 @@ Accel build_accel(const Scene &sc, int json_shapes) {
         const int root = b.emit(rest, 0, rest.size());
         a.nodes.reserve(b.tree.size() * BVH_OCTANTS);
         for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());
+    }
+    a.cnodes.reserve(a.nodes.size());
+    for (const DNode &n : a.nodes) {
+        if (n.first < 0 || n.first >= (1 << 24) || n.count < 0 || n.count > 255)
+            throw std::runtime_error("BVH too large for the compact node form (leaf index >= 2^24)");
+        DNodeC c{};
+        for (int k = 0; k < 3; k++) {
+            float lo = (float)n.lo[k], hi = (float)n.hi[k];
+            if ((double)lo > n.lo[k]) lo = std::nextafter(lo, -INFINITY);
+            if ((double)hi < n.hi[k]) hi = std::nextafter(hi, INFINITY);
+            c.lo[k] = lo;
+            c.hi[k] = hi;
+        }
+        c.skip = n.skip;
+        c.first_count = (uint32_t)n.first | (uint32_t)n.count << 24;
+        a.cnodes.push_back(c);
     }
     return a;
 }

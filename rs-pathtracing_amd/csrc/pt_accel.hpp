@@ -31,6 +31,7 @@ namespace pt {
 constexpr int BVH_OCTANTS = 8;
 struct Accel {
     std::vector<DNode> nodes;    // BVH_OCTANTS layouts of nodes_per_octant() nodes each
+    std::vector<DNodeC> cnodes;  // the same nodes in the device form (f32 boxes rounded outward)
     int nodes_per_octant() const { return (int)(nodes.size() / BVH_OCTANTS); }
     std::vector<int32_t> leaf;   // shape ids referenced by leaf nodes
     std::vector<int32_t> lin;    // wave-uniform list

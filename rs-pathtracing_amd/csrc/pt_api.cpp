@@ -206,7 +206,7 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
     };
     upload(&r->ds.shapes, hs);
     upload(&r->ds.mats, hm);
-    upload(&r->ds.nodes, acc.nodes);
+    upload(&r->ds.nodes, acc.cnodes);
     upload(&r->ds.leaf, acc.leaf);
     upload(&r->ds.lin, acc.lin);
     upload(&r->ds.march, acc.march);

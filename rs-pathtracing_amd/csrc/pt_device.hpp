@@ -254,7 +254,7 @@ PT_HD DBox uniform_box(const DBox *p) {
 struct Scene {
     const DShape *__restrict__ shapes;
     const DMaterial *__restrict__ mats;
-    const DNode *__restrict__ nodes;
+    const DNodeC *__restrict__ nodes;  // compact form (pt_types.hpp)
     const int32_t *__restrict__ leaf;
     const int32_t *__restrict__ lin;
     const int32_t *__restrict__ march;
@@ -308,15 +308,17 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     }
     // threaded BVH over the remaining non-marched shapes, in the layout of the
     // ray's direction octant (near child first, pt_accel.hpp)
-    const DNode *nodes = sc.nodes + (size_t)((r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0)) *
+    const DNodeC *nodes = sc.nodes + (size_t)((r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0)) *
                                         (size_t)sc.nnodes;
     int n = 0;
     while (n < sc.nnodes) {
-        const DNode &nd = nodes[n];
+        const DNodeC nd = nodes[n];
         if (STATS) ct->c[C_NODE_SLABS]++;
-        if (slab(nd.lo, nd.hi, r, inv, min_t, best)) {
-            for (int k = 0; k < nd.count; k++) {
-                int i = sc.leaf[nd.first + k];
+        const double lo[3] = {nd.lo[0], nd.lo[1], nd.lo[2]}, hi[3] = {nd.hi[0], nd.hi[1], nd.hi[2]};
+        if (slab(lo, hi, r, inv, min_t, best)) {
+            const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24);
+            for (int k = 0; k < count; k++) {
+                int i = sc.leaf[first + k];
                 double t;
                 if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
                     best = t;

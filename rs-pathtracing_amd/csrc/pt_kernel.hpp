@@ -10,7 +10,7 @@ namespace pt {
 struct DeviceScene {
     DShape *shapes = nullptr;
     DMaterial *mats = nullptr;
-    DNode *nodes = nullptr;
+    DNodeC *nodes = nullptr;
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     DTexture *tex = nullptr;  // non-solid textures (null when the scene has none)

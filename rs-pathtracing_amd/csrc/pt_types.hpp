@@ -59,6 +59,19 @@ struct alignas(64) DNode {
 };
 static_assert(sizeof(DNode) == 64, "DNode is one cache line");
 
+// The device form of a DNode, half a cache line: the f64 box rounded outward
+// to f32 (so its f64 slab test accepts a superset of the exact box's rays:
+// rounding is monotone, and the exact leaf tests still decide every hit, in
+// the order-independent tie rule of closest_nomarch), skip as in DNode, and
+// first | count << 24 (leaves hold at most 16 shapes; first < 2^24 is checked
+// when the BVH is built).
+struct alignas(32) DNodeC {
+    float lo[3], hi[3];
+    int32_t skip;
+    uint32_t first_count;
+};
+static_assert(sizeof(DNodeC) == 32, "DNodeC is half a cache line");
+
 struct DBox {
     double lo[3], hi[3];
 };

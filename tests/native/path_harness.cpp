@@ -30,7 +30,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         for (auto &m : b->sc.materials) b->mats.push_back(to_device(m));
         b->view.shapes = b->shapes.data();
         b->view.mats = b->mats.data();
-        b->view.nodes = b->acc.nodes.data();
+        b->view.nodes = b->acc.cnodes.data();
         b->view.leaf = b->acc.leaf.data();
         b->view.lin = b->acc.lin.data();
         b->view.march = b->acc.march.data();

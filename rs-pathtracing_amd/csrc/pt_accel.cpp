@@ -196,7 +196,11 @@ Accel build_accel(const Scene &sc, int json_shapes) {
             c.hi[k] = hi;
         }
         c.skip = n.skip;
-        c.first_count = (uint32_t)n.first | (uint32_t)n.count << 24;
+        // a one-shape leaf holds the shape id itself (bit 31), saving the dependent leaf[] load
+        if (n.count == 1 && a.leaf[n.first] >= 0 && a.leaf[n.first] < (1 << 24))
+            c.first_count = (uint32_t)a.leaf[n.first] | 1u << 24 | 1u << 31;
+        else
+            c.first_count = (uint32_t)n.first | (uint32_t)n.count << 24;
         a.cnodes.push_back(c);
     }
     return a;

@@ -316,9 +316,10 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
         if (STATS) ct->c[C_NODE_SLABS]++;
         const double lo[3] = {nd.lo[0], nd.lo[1], nd.lo[2]}, hi[3] = {nd.hi[0], nd.hi[1], nd.hi[2]};
         if (slab(lo, hi, r, inv, min_t, best)) {
-            const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24);
+            const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24 & 0x7fu);
+            const bool direct = nd.first_count >> 31;  // one-shape leaf: `first` is the shape id
             for (int k = 0; k < count; k++) {
-                int i = sc.leaf[first + k];
+                int i = direct ? first : sc.leaf[first + k];
                 double t;
                 if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
                     best = t;

@@ -11,11 +11,13 @@ enum ShapeKind : int32_t { SPHERE = 0, RECTANGLE = 1, CUBE = 2, MARCH = 3, TORUS
 enum MaterialKind : int32_t { LAMBERTIAN = 0, METAL = 1, DIELECTRIC = 2, DIFFUSE_LIGHT = 3, EMPTY = 4 };
 
 struct alignas(64) DShape {
-    double inv[12];  // InversableTransform::inverse, rows 0..2 (3x4)
-    double dir[12];  // InversableTransform::direct, rows 0..2
-    double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step | Torus radius, tube_radius
+    // a miss test of a sphere or cube reads only the first two cache lines
+    // (type + inv); rectangles add the third (p)
     int32_t type, material, inverse_normal, depth;
+    double inv[12];  // InversableTransform::inverse, rows 0..2 (3x4)
     int32_t func, pad[3];
+    double p[4];     // Rectangle x0,y0,x1,y1 | RayMarchingShape: step | Torus radius, tube_radius
+    double dir[12];  // InversableTransform::direct, rows 0..2
     double fk[4];    // RayMarchingShape function constants (pt_funcs.hpp FParams::k)
     double fradius;  // its bound's sphere_radius
     double pad2[3];
@@ -64,7 +66,8 @@ static_assert(sizeof(DNode) == 64, "DNode is one cache line");
 // rounding is monotone, and the exact leaf tests still decide every hit, in
 // the order-independent tie rule of closest_nomarch), skip as in DNode, and
 // first | count << 24 (leaves hold at most 16 shapes; first < 2^24 is checked
-// when the BVH is built).
+// when the BVH is built); bit 31 marks a one-shape leaf whose `first` is the
+// shape id itself rather than an index into the leaf list.
 struct alignas(32) DNodeC {
     float lo[3], hi[3];
     int32_t skip;

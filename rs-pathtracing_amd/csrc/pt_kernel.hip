@@ -23,7 +23,7 @@ using dev::Ray;
 using dev::V3;
 
 // WAVES = minimum waves per SIMD the register allocation must allow
-// (__launch_bounds__' second argument): 2 -> <= 256 VGPRs, 3 -> <= 168, 4 -> <= 128.
+// (__launch_bounds__' second argument): 2 -> <= 256 VGPRs, 3 -> <= 168, 4 -> <= 128, 5 -> <= 102.
 template <int NW, int WAVES, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
     const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
@@ -242,14 +242,14 @@ static dev::Scene dscene(const DeviceScene &s) {
         }                                  \
     } while (0)
 
-// Occupancy variant of render_tiles (PT_WAVES=2|3|4 in the environment, read
+// Occupancy variant of render_tiles (PT_WAVES=2|3|4|5 in the environment, read
 // once; default below).  Depths > 8 use the 2-wave build: their attenuation
 // stacks are wider.
 static int render_waves() {
     static int w = [] {
         const char *e = getenv("PT_WAVES");
         int v = e ? atoi(e) : PT_DEFAULT_WAVES;
-        return (v >= 2 && v <= 4) ? v : PT_DEFAULT_WAVES;
+        return (v >= 2 && v <= 5) ? v : PT_DEFAULT_WAVES;
     }();
     return w;
 }
@@ -277,6 +277,7 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
         switch (render_waves()) {
         case 2: render_tiles<4, 2, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         case 3: render_tiles<4, 3, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
+        case 5: render_tiles<4, 5, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         default: render_tiles<4, 4, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         }
     } else if (P.depth <= 8) {

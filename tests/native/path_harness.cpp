@@ -59,6 +59,28 @@ extern "C" void h_accel_stats(void *p, int *out) {
     out[3] = (int)b->acc.leaf.size();
 }
 
+// Device node form against the host nodes: each f32 box must contain the f64
+// box, skip must match, and first/count must decode to the same leaf shapes.
+// Returns the number of nodes that fail (0 expected).
+extern "C" int h_node_check(void *p) {
+    Bundle *b = (Bundle *)p;
+    const auto &N = b->acc.nodes;
+    const auto &Cn = b->acc.cnodes;
+    if (N.size() != Cn.size()) return -1;
+    int bad = 0;
+    for (size_t i = 0; i < N.size(); i++) {
+        bool ok = Cn[i].skip == N[i].skip;
+        for (int k = 0; k < 3; k++) ok = ok && (double)Cn[i].lo[k] <= N[i].lo[k] && (double)Cn[i].hi[k] >= N[i].hi[k];
+        const uint32_t fc = Cn[i].first_count;
+        const int count = (int)(fc >> 24 & 0x7fu), first = (int)(fc & 0xffffffu);
+        ok = ok && count == N[i].count;
+        if (fc >> 31) ok = ok && count == 1 && first == b->acc.leaf[N[i].first];
+        else ok = ok && first == N[i].first;
+        bad += !ok;
+    }
+    return bad;
+}
+
 extern "C" int h_closest(void *p, const double *ray, double min_t, double max_t, double *t, double *point,
                          double *normal, int *front) {
     Bundle *b = (Bundle *)p;

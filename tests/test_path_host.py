@@ -24,6 +24,7 @@ def H():
     L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]
     L.h_scene_free.argtypes = [C.c_void_p]
     L.h_accel_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    L.h_node_check.argtypes = [C.c_void_p]
     L.h_closest.argtypes = [C.c_void_p, d, C.c_double, C.c_double, d, d, d, C.POINTER(C.c_int)]
     L.h_ray_color.argtypes = [C.c_void_p, d, C.POINTER(C.c_uint64), C.c_uint32, d]
     L.h_trace_pixels.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
@@ -75,6 +76,12 @@ def test_accel_layout(H, cornell):
     nodes, nlin, nmarch, nleaf = list(st)
     assert nlin == 8 and nmarch == 1  # 6 rectangles + 2 cubes uniform; the Heart marched last
     assert nleaf == cornell.o.num_shapes - 9  # every random sphere sits in the BVH once
+
+
+def test_compact_nodes_contain_host_boxes(H, cornell):
+    # DNodeC (pt_types.hpp): f32 boxes rounded outward must contain the f64 boxes, and the packed
+    # first/count (or the direct shape id of a one-shape leaf) must decode to the host node's leaf
+    assert H.h_node_check(cornell.h) == 0
 
 
 def test_closest_hit_matches_oracle(cornell):

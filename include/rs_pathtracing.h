@@ -140,8 +140,9 @@ int pt_render_stop(pt_renderer *r);
 /* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */
 /* Renders this rank's share of the frame straight into device memory on
  * `hip_stream` (a hipStream_t; 0 = the null stream, as in every HIP call and
- * in pt_unshard_device).  Pixels are cut into 16x16 tiles
- * numbered row-major; tile k belongs to rank k % world.  world == 1: d_out is
+ * in pt_unshard_device).  Pixels are cut into 16x16 tiles; logical tile k belongs to rank k % world and sits in
+ * tile row k / tiles_x at column (k % tiles_x + row) % tiles_x (a diagonal
+ * deal, so a rank's columns change from row to row).  world == 1: d_out is
  * the w*h*3 frame.  world > 1: d_out holds this rank's tiles in order,
  * pt_shard_tiles(...) * 256 * 3 doubles (pixels outside the frame are 0). */
 int pt_render_device(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,

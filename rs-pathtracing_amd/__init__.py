@@ -423,11 +423,16 @@ def shard_tiles(width: int, height: int, rank: int, world: int) -> int:
 
 def shard_pixels(width: int, height: int, rank: int, world: int) -> np.ndarray:
     """Pixel index (x + y*w) of each slot of rank's compact shard, -1 outside
-    the frame: tile k (16x16, row-major tiles) belongs to rank k % world, tiles
-    in order, pixels row-major inside a tile (render_tiles' layout)."""
+    the frame: logical tile k (16x16) belongs to rank k % world, tiles in
+    order, pixels row-major inside a tile (render_tiles' layout).  For world > 1
+    logical tile k sits at column (k % tiles_x + row) % tiles_x of its row
+    (dev::tile_position, a diagonal deal); world == 1 is row-major."""
     tx = (width + TILE - 1) // TILE
     ty = (height + TILE - 1) // TILE
     k = np.arange(rank, tx * ty, world)
+    if world > 1:
+        row = k // tx
+        k = row * tx + (k % tx + row) % tx
     ly, lx = np.divmod(np.arange(TILE * TILE), TILE)
     x = (k % tx)[:, None] * TILE + lx[None, :]
     y = (k // tx)[:, None] * TILE + ly[None, :]

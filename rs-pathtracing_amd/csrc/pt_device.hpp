@@ -251,6 +251,21 @@ PT_HD DBox uniform_box(const DBox *p) {
     return b;
 }
 
+// Multi-rank tile deal (world > 1): rank r owns logical tiles k = r + i*world;
+// logical tile k sits at column (k % tiles_x + row) % tiles_x of its row, so a
+// rank's columns shift by one per row (a diagonal deal) instead of repeating
+// in every row when tiles_x is a multiple of world.  world == 1: identity.
+PT_HD inline uint32_t tile_position(uint32_t k, uint32_t tiles_x, uint32_t world) {
+    if (world <= 1) return k;
+    const uint32_t ty = k / tiles_x;
+    return ty * tiles_x + (k % tiles_x + ty) % tiles_x;
+}
+PT_HD inline uint32_t tile_logical(uint32_t p, uint32_t tiles_x, uint32_t world) {
+    if (world <= 1) return p;
+    const uint32_t ty = p / tiles_x;
+    return ty * tiles_x + (p % tiles_x + tiles_x - ty % tiles_x) % tiles_x;
+}
+
 struct Scene {
     const DShape *__restrict__ shapes;
     const DMaterial *__restrict__ mats;

@@ -27,7 +27,7 @@ using dev::V3;
 template <int NW, int WAVES, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
     const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
-    const uint32_t k = P.rank + ti * P.world;       // global tile id
+    const uint32_t k = dev::tile_position(P.rank + ti * P.world, P.tiles_x, P.world);  // global tile id
     const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t lx = ((w & 1u) << 3) | (l & 7u), ly = ((w >> 1) << 3) | (l >> 3);
@@ -49,7 +49,7 @@ __global__ void unshard(const double *__restrict__ g, uint32_t width, uint32_t h
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (size_t)width * height) return;
     uint32_t x = (uint32_t)(i % width), y = (uint32_t)(i / width);
-    uint32_t k = (y / TILE) * tiles_x + x / TILE;
+    uint32_t k = dev::tile_logical((y / TILE) * tiles_x + x / TILE, tiles_x, world);
     uint32_t rank = k % world, ti = k / world;
     const double *s = g + (((size_t)rank * per_rank + ti) * (TILE * TILE) + (y % TILE) * TILE + x % TILE) * 3;
     frame[i * 3 + 0] = s[0];
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void march_probe(const double *__restrict__ jo
 __global__ __launch_bounds__(256, 2) void render_tiles_timed(dev::Scene sc, FrameParams P, double *__restrict__ out,
                                                              unsigned long long *__restrict__ acc) {
     const uint32_t ti = P.tile_begin + blockIdx.x;
-    const uint32_t k = P.rank + ti * P.world;
+    const uint32_t k = dev::tile_position(P.rank + ti * P.world, P.tiles_x, P.world);
     const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint32_t lx = ((w & 1u) << 3) | (l & 7u), ly = ((w >> 1) << 3) | (l >> 3);

@@ -133,7 +133,7 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
     *pix_local = within;
     const uint32_t ti = v.tile0 + within / (TILE * TILE);
     const uint32_t th = within % (TILE * TILE);
-    const uint32_t k = P.rank + ti * P.world;
+    const uint32_t k = dev::tile_position(P.rank + ti * P.world, P.tiles_x, P.world);
     const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;
     const uint32_t w = th >> 6, l = th & 63;
     *x = tx * TILE + (((w & 1u) << 3) | (l & 7u));

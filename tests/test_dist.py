@@ -1,5 +1,5 @@
 """Multi-GPU path on the CPU: world_size 2 over gloo.  Each rank renders its
-tile shard (tile k -> rank k % world, the render_tiles layout) with the CPU
+tile shard (logical tile k -> rank k % world, dealt diagonally; the render_tiles layout) with the CPU
 oracle, the shards are gathered to rank 0 with torch.distributed, and the
 frame is rebuilt with the host mirror of pt_unshard_device.  The result must
 equal the single-process render bit for bit (per-(pixel, sample) RNG keys

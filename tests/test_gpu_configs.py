@@ -119,3 +119,28 @@ def test_c5_synthetic_100k_spheres(pt, c5):
     ref = osc.render(160, 90, 2, 8, 2)
     assert np.array_equal(img, ref)
     assert img.mean() > 0.05
+
+
+def test_shard_pixels_matches_device_deal(pt, cornell):
+    # the host map (shard_pixels, used by unshard_host) and the kernels' diagonal deal
+    # (dev::tile_position) place every shard slot on the same frame pixel
+    import torch
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h, spp, world = 200, 72, 1, 4   # ragged edge tiles, 13 tiles per row
+    stream = torch.cuda.current_stream().cuda_stream
+    full = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    r.render_device(cam, w, h, spp, 9, 0, 1, full.data_ptr(), stream)
+    per = pt.shard_tiles(w, h, 0, world)
+    full_h = None
+    for rank in range(world):
+        s = torch.zeros(per * 256 * 3, dtype=torch.float64, device="cuda")
+        r.render_device(cam, w, h, spp, 9, rank, world, s.data_ptr(), stream)
+        torch.cuda.synchronize()
+        if full_h is None:
+            full_h = full.view(-1, 3).cpu().numpy()
+        idx = pt.shard_pixels(w, h, rank, world)
+        got = s.view(-1, 3).cpu().numpy()[: len(idx)]
+        ok = idx >= 0
+        assert np.array_equal(got[ok], full_h[idx[ok]])

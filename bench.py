@@ -1,7 +1,8 @@
 """Benchmark: Msamples/s on cornell_box 1920x1080, 256 spp, 8 bounces (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+    python bench.py --gpus N --single-process      # N devices behind one pt_renderer_create_multi
 
 One step = one full frame (all W*H*spp camera samples, every bounce) rendered
 from scene data resident in HBM into an HBM frame buffer.  For N > 1 the
@@ -9,10 +10,20 @@ frame's 16x16 tiles are dealt round-robin to the ranks (tile k -> rank k % N),
 each rank renders its tiles into a compact shard, the shards are gathered to
 rank 0 over RCCL (torch.distributed "nccl") and un-interleaved there: the same
 frame at every N ("scaling": "strong").  Rank 0 prints one JSON line.
+
+After the timed steps (not part of `value`):
+* roofline: one more frame with one chunk stream (wf_slots = 1), so every
+  render kernel runs alone and its HIP-event launch durations are its own; the
+  dominant kernel's algorithmic FLOPs per launch / its mean launch duration.
+  The timed steps run two chunk streams, whose kernels overlap (their summed
+  durations exceed the frame time), so the whole path's rate is reported too.
+* parity: >= 8192 stratified pixels (a 16-pixel grid plus a full row and a full
+  column through the Heart) against the oracle at the full spp;
+* cpu_baseline: the oracle in the reference's BvhNode mode, on the host's
+  cores (this process's CPU share) and on the reference's 12 threads.
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -24,6 +35,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Msamples/sec cornell_box 1920x1080x256spp at 1/2/4/8 MI355X; RMS pixel delta"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (FMA = 2 FLOP); no-FMA instruction peak is half of it
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
+REF_THREADS = 12          # the reference GUI's ThreadPoolRenderer::new(scene, 12, 50) (src/bin/main.rs:229-239)
 
 # FLOPs per event of the kernels' own traversal (counted in pt_device.hpp /
 # pt_march.hpp; f64 add/sub/mul/div/sqrt = 1 FLOP, compares, min/max and
@@ -53,10 +65,11 @@ def flops_per_sample(cnt, keys=None):
     return sum(FLOP_WEIGHTS[k] * cnt[k] for k in keys) / max(1, cnt["samples"])
 
 
-# BASELINE.json configs[1..4] (configs[0] is the reference's own CPU case):
-# scene, width, height, spp.  c2 is the headline (the default); c5's scene is
-# generated (scenes/make_scenes.py synthetic(100000)), not a file.
+# BASELINE.json configs: scene, width, height, spp.  c1 is the reference's own
+# CPU-runnable case (spheres.json, the GUI's scene), c2 the headline (the
+# default); c5's scene is generated (scenes/make_scenes.py synthetic(100000)).
 CONFIGS = {
+    "c1": ("spheres.json", 256, 256, 16),
     "c2": ("cornell_box.json", 1920, 1080, 256),
     "c3": ("cornell_box.json", 3840, 2160, 1024),
     "c4": ("cornell_box.json", 3840, 2160, 4096),
@@ -86,23 +99,60 @@ def parse():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--scene-seed", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--slots", type=int, default=None, help="chunk streams in flight (renderer default: 2)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N GPUs behind one renderer (pt_renderer_create_multi, peer-copy gather) instead of ranks")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of each CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--parity-pixels", type=int, default=48)
+    ap.add_argument("--no-roofline-leg", action="store_true", help="skip the one-stream roofline frame")
+    ap.add_argument("--parity-pixels", type=int, default=0,
+                    help="0: the stratified set (>= 8192 pixels); n: n random pixels")
     a = ap.parse_args()
     if a.config:
         a.scene, a.width, a.height, a.spp = CONFIGS[a.config]
     return a
 
 
-def cpu_baseline(text, args, threads):
-    """The oracle in the reference's BvhNode mode (the reference threaded
-    renderer's algorithm, step_by_step chunking) on a bounded sample: the full
-    frame at k spp, k chosen from a probe so the run takes ~cpu_seconds."""
+def metric_name(args):
+    if (args.scene, args.width, args.height, args.spp, args.depth) == ("cornell_box.json", 1920, 1080, 256, 8):
+        return METRIC
+    return "Msamples/sec %s %dx%dx%dspp depth %d" % (args.scene.replace(".json", ""), args.width, args.height,
+                                                    args.spp, args.depth)
+
+
+def host_cpus():
+    """The host's CPUs as this process sees them: the model, nproc, the affinity
+    mask, a cgroup CPU quota and OMP_NUM_THREADS; `share` is the smallest, the
+    threads the CPU baseline may use (the GPU box grants one GPU's share of a
+    machine whose os.cpu_count() shows every CPU)."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["nproc"]
+    try:
+        q = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        info["cgroup_cpus"] = None if q[0] == "max" else round(int(q[0]) / int(q[1]), 2)
+    except (OSError, ValueError, IndexError):
+        info["cgroup_cpus"] = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    info["omp_num_threads"] = int(omp) if omp and omp.isdigit() else None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cands = [info["affinity"]] + [int(v) for v in (info["cgroup_cpus"], info["omp_num_threads"]) if v]
+    info["share"] = max(1, min(cands))
+    return info
+
+
+def time_oracle(sc, args, threads):
+    """Full frames at k spp, k from a probe so the run takes ~cpu_seconds."""
     import numpy as np
-    import oracle
-    sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
     w, h = args.width, args.height
     px = (np.arange(0, h, 4)[:, None] * w + np.arange(0, w, 4)[None, :]).ravel().astype(np.uint32)
     t = time.perf_counter()
@@ -113,9 +163,27 @@ def cpu_baseline(text, args, threads):
     sc.render(w, h, spp, args.depth, args.seed, threads=threads)
     dt = time.perf_counter() - t
     n = w * h * spp
-    return {"value": round(n / dt / 1e6, 6), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "full %dx%d frame at %d spp, depth %d = %d samples in %.1f s (%d threads); oracle "
-                      "restatement with the reference's BvhNode traversal" % (w, h, spp, args.depth, n, dt, threads)}
+    return n / dt / 1e6, spp, n, dt
+
+
+def cpu_baseline(text, args):
+    """The oracle in the reference's BvhNode mode (the reference threaded
+    renderer's algorithm, step_by_step chunking, src/renderer/mod.rs:66-125) on
+    a bounded sample: the full frame at k spp.  Timed on this process's CPU
+    share and on the reference GUI's 12 threads."""
+    import oracle
+    host = host_cpus()
+    sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
+    v, spp, n, dt = time_oracle(sc, args, host["share"])
+    v12, spp12, n12, dt12 = time_oracle(sc, args, REF_THREADS)
+    what = "oracle restatement with the reference's BvhNode traversal"
+    return {"value": round(v, 6), "unit": "Msamples/s", "cores": host["share"], "kind": "port",
+            "sample": "full %dx%d frame at %d spp, depth %d = %d samples in %.1f s (%d threads); %s"
+                      % (args.width, args.height, spp, args.depth, n, dt, host["share"], what),
+            "ref_threads": {"value": round(v12, 6), "cores": REF_THREADS,
+                            "sample": "full frame at %d spp = %d samples in %.1f s (12 threads, the reference GUI's)"
+                                      % (spp12, n12, dt12)},
+            "host": host}
 
 
 def algorithmic_flops(pt, r, cam, args):
@@ -128,6 +196,32 @@ def algorithmic_flops(pt, r, cam, args):
     return flops_per_sample(cnt), cnt
 
 
+def parity_pixels(args):
+    """A 16-pixel grid over the frame plus a full row and a full column through
+    the Heart (cornell's heaviest rays: y ~ 757/1080, x ~ 1142/1920 of the
+    frame), or n random pixels."""
+    import numpy as np
+    W, H = args.width, args.height
+    if args.parity_pixels:
+        rng = np.random.default_rng(1234)
+        return rng.choice(W * H, size=min(args.parity_pixels, W * H), replace=False).astype(np.uint32)
+    grid = (np.arange(7, H, 16)[:, None] * W + np.arange(7, W, 16)[None, :]).ravel()
+    yr, xc = min(H - 1, H * 757 // 1080), min(W - 1, W * 1142 // 1920)
+    row = yr * W + np.arange(W)
+    col = np.arange(H) * W + xc
+    return np.unique(np.concatenate([grid, row, col])).astype(np.uint32)
+
+
+def traffic_file(workload):
+    for rnd in ("r2", "r1"):
+        f = ROOT / "profiles" / rnd / "pmc_traffic_c2.json"
+        if f.exists():
+            tr = json.loads(f.read_text())
+            if tr.get("workload") == workload:
+                return f, tr
+    return None, None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -137,7 +231,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
+    multi = args.single_process and world == 1 and args.gpus > 1
+    if world != args.gpus and rank == 0 and not multi:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
@@ -147,12 +242,19 @@ def main():
     pt = ge.load_package()
     text = scene_text(args.scene)
     scene = pt.Scene.from_json(text, seed=args.scene_seed)
-    r = pt.HipRenderer(scene, device=local, depth=args.depth)
+    if multi:
+        r = pt.HipRenderer(scene, depth=args.depth, devices=list(range(args.gpus)))
+    else:
+        r = pt.HipRenderer(scene, device=local, depth=args.depth)
+    if args.slots:
+        r.set_option("wf_slots", args.slots)
+    slots = r.get_option("wf_slots")
     cam = scene.camera()
     W, H, spp = args.width, args.height, args.spp
     stream = torch.cuda.Stream()  # a real stream: the HIP events below time exactly our launches
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    n_gpus = args.gpus if multi else world
 
     frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
     per = pt.shard_tiles(W, H, 0, world)
@@ -167,7 +269,9 @@ def main():
     def step():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
-        if world == 1:
+        if multi:
+            r.render_frame_device(cam, W, H, spp, args.seed, frame.data_ptr(), sp)
+        elif world == 1:
             r.render_device(cam, W, H, spp, args.seed, 0, 1, frame.data_ptr(), sp)
         else:
             r.render_device(cam, W, H, spp, args.seed, rank, world, shard.data_ptr(), sp)
@@ -177,11 +281,12 @@ def main():
         if world > 1:
             dist.gather(shard, glist, dst=0)
             if rank == 0:
-                pt.unshard_device(gathered.data_ptr(), W, H, world, frame.data_ptr(), sp)
+                pt.unshard_device(gathered.data_ptr(), W, H, world, frame.data_ptr(), sp, device=local)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    pt.march_guard_drops(r)  # clear
     k_start.clear()
     k_end.clear()
     pt.kernel_timing(r, True)  # per-kernel HIP events on the launch stream, timed steps only
@@ -196,6 +301,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kt = pt.kernel_timing(r, False)
+    guard_drops = pt.march_guard_drops(r)
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
@@ -204,72 +310,116 @@ def main():
     else:
         kernel_ms_max = kernel_ms
 
+    # roofline leg: one frame with every render kernel alone on the device (one chunk stream)
+    kt_iso = None
+    if not args.no_roofline_leg:
+        r.set_option("wf_slots", 1)
+        pt.kernel_timing(r, True)
+        if multi:
+            r.render_frame_device(cam, W, H, spp, args.seed, frame.data_ptr(), sp)
+        else:
+            r.render_device(cam, W, H, spp, args.seed, rank, world, (shard if world > 1 else frame).data_ptr(), sp)
+        torch.cuda.synchronize()
+        kt_iso = pt.kernel_timing(r, False)
+        r.set_option("wf_slots", slots)
+        if world > 1:  # the last timed frame is what rank 0 checks: render it again
+            step()
+            torch.cuda.synchronize()
+
     if rank == 0:
         samples_frame = W * H * spp
         value = samples_frame * args.steps / elapsed / 1e6
         img = frame.view(-1, 3).cpu().numpy()
         sys.path.insert(0, str(ROOT / "oracle"))
-        threads = min(16, os.cpu_count() or 1)
 
-        # roofline of the dominant kernel, this rank's launches in the timed steps
+        # roofline of the dominant kernel (this rank's / the first device's launches)
         F, counts = algorithmic_flops(pt, r, cam, args)
-        my_tiles = pt.shard_tiles(W, H, rank, world)
-        samples_rank = samples_frame * my_tiles / (pt.shard_tiles(W, H, 0, 1)) * args.steps
+        share = 1.0 if multi else pt.shard_tiles(W, H, rank, world) / pt.shard_tiles(W, H, 0, 1)
+        if multi:  # kernel timing covers the first device: its tile share
+            share = pt.shard_tiles(W, H, 0, args.gpus) / pt.shard_tiles(W, H, 0, 1)
+        samples_share = samples_frame * share
         f_kind = {"march": flops_per_sample(counts, MARCH_EVENTS),
                   "bounce": flops_per_sample(counts, [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS]),
                   "megakernel": F}
-        dom = max(("bounce", "march", "megakernel"), key=lambda k: kt[k][0])
-        dom_ms, dom_n = kt[dom]
-        achieved = f_kind[dom] * samples_rank / (dom_ms / 1e3) / 1e12
-        out_bytes = 24.0 * W * H * my_tiles / pt.shard_tiles(W, H, 0, 1)
+        kname = {"bounce": "wf_bounce", "march": "wf_march", "megakernel": "render_tiles"}
+        src = kt_iso if kt_iso is not None else kt
+        nfr = 1 if kt_iso is not None else args.steps
+        dom = max(("bounce", "march", "megakernel"), key=lambda k: src[k][0])
+        dom_ms, dom_n = src[dom]
+        achieved = f_kind[dom] * samples_share * nfr / (dom_ms / 1e3) / 1e12
+        per_kernel = {}
+        for k in ("bounce", "march", "megakernel"):
+            ms_k, n_k = src[k]
+            if n_k:
+                a_k = f_kind[k] * samples_share * nfr / (ms_k / 1e3) / 1e12
+                per_kernel[kname[k]] = {"achieved": round(a_k, 4), "frac": round(a_k / FP64_PEAK_TFLOPS, 5),
+                                        "flops_per_sample": round(f_kind[k], 1), "launches": n_k // nfr,
+                                        "ms_per_frame": round(ms_k / nfr, 3),
+                                        "kernel_ms_avg": round(ms_k / n_k, 4)}
+        out_bytes = 24.0 * W * H * share
+        workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
+        tuning = {k: v for k, v in r.options().items() if v != pt.OPTION_DEFAULTS.get(k)}
         rec = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world,
+            "metric": metric_name(args), "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n_gpus,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: re-authored %s, add_random_spheres from seed %d" % (args.scene, args.scene_seed),
-            "config": {"workload": "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth),
+            "config": {"workload": workload, "config": args.config or ("c2" if metric_name(args) == METRIC else None),
                        "width": W, "height": H, "spp": spp, "depth": args.depth, "seed": args.seed,
-                       "parallelism": "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"},
+                       "parallelism": ("%d devices in one process, peer-copy gather" % args.gpus if multi else
+                                       "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"),
+                       "wf_slots": slots},
             "roofline": {"bound": "valu_f64", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5), "traffic": None,
-                         "kernel": "wf_" + dom if dom != "megakernel" else "render_tiles",
-                         "flops_per_sample": round(f_kind[dom], 1), "launches": dom_n,
-                         "kernel_ms_avg": round(dom_ms / max(1, dom_n), 4),
-                         "kernel_ms_by_kind": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+                         "kernel": kname[dom], "flops_per_sample": round(f_kind[dom], 1),
+                         "launches": dom_n // nfr, "kernel_ms_avg": round(dom_ms / max(1, dom_n), 4),
+                         "measured": ("one extra frame after the timed steps with one chunk stream (wf_slots=1): "
+                                      "every launch alone on the device, HIP events on its stream"
+                                      if kt_iso is not None else "timed steps (launches of two chunk streams overlap)"),
+                         "kernels": per_kernel,
                          "flops_per_sample_total": round(F, 1),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},
+                         # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
+                         # launches overlap the other kind's; the whole path's rate is the frame's FLOPs over
+                         # the frame time
+                         "timed_kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
                          "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3),
-                         # two chunks run concurrently (pt_wave.hip), so one kernel's launches overlap the
-                         # other kind's: the whole path's rate is the frame's FLOPs over the frame time
                          "path_achieved": round(F * value * 1e6 / 1e12, 4),
                          "path_frac": round(F * value * 1e6 / 1e12 / FP64_PEAK_TFLOPS, 5)},
             "roofline_hbm": {"achieved": round(out_bytes / (kernel_ms / 1e3) / 1e9, 4), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
+            "march_guard_drops": guard_drops,
         }
+        if tuning:
+            rec["tuning"] = tuning
         # roofline.traffic: HBM bytes per launch of the same kernel from the committed PMC passes of this
         # workload (scripts/pmc_traffic.py; bench.py cannot read PMC counters itself)
-        tfile = ROOT / "profiles" / "r1" / "pmc_traffic_c2.json"
-        if tfile.exists():
-            tr = json.loads(tfile.read_text())
+        tf, tr = traffic_file(workload)
+        if tr and world == 1 and not multi:
             kind = tr.get("kinds", {}).get(dom)
-            if tr.get("workload") == rec["config"]["workload"] and kind and world == 1:
+            if kind:
                 rec["roofline"]["traffic"] = round(kind["traffic"])
-                rec["roofline"]["traffic_source"] = "profiles/r1/pmc_traffic_c2.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+                rec["roofline"]["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % tf.relative_to(ROOT)
                 rec["roofline"]["traffic_gbs"] = round(kind["traffic"] / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
         if not args.no_parity:
             import oracle
-            rng = np.random.default_rng(1234)
-            px = rng.choice(W * H, size=args.parity_pixels, replace=False).astype(np.uint32)
+            px = parity_pixels(args)
             sc = oracle.Scene(text, seed=args.scene_seed).use_bvh(True, 7)
-            ref = sc.render(W, H, spp, args.depth, args.seed, pixels=px, threads=threads)
+            t = time.perf_counter()
+            ref = sc.render(W, H, spp, args.depth, args.seed, pixels=px, threads=host_cpus()["share"])
             got = img[px]
             rec["rms_vs_oracle"] = float(np.sqrt(np.mean((got - ref) ** 2)))
+            rec["rms_per_channel"] = [float(x) for x in np.sqrt(np.mean((got - ref) ** 2, axis=0))]
             rec["rms_pixels"] = int(len(px))
             rec["exact_pixels_frac"] = float(np.mean(np.all(got == ref, axis=1)))
+            rec["parity_pixels"] = ("stratified: 16-px grid + full row %d + full column %d, %d spp, %.1f s"
+                                    % (min(H - 1, H * 757 // 1080), min(W - 1, W * 1142 // 1920), spp,
+                                       time.perf_counter() - t) if not args.parity_pixels
+                                    else "%d random pixels" % len(px))
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(text, args, threads)
+            rec["cpu_baseline"] = cpu_baseline(text, args)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

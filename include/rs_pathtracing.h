@@ -124,9 +124,37 @@ int pt_camera_new(const double position[3], const double direction[3], const dou
  * (src/renderer/step_by_step.rs:37): `device` (HIP ordinal, -1 = current)
  * replaces thread_number.  The scene must outlive the renderer. */
 int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer **out);
+/* The same constructor with the parallelism knob spread over GPUs (the
+ * thread_number of step_by_step.rs:37 -> ngpu): devices[0..ngpu) are HIP
+ * ordinals (NULL: 0 .. ngpu-1; ngpu <= 0 with NULL devices: every visible
+ * device; an ordinal may repeat, e.g. to rehearse the deal on one GPU).
+ * Each device gets its own copy of the scene and its own stream.  A frame's
+ * 16x16 tiles are dealt to the devices as to the ranks of pt_render_device
+ * (logical tile k -> device k % ngpu, diagonal deal); each device renders
+ * its tiles into a compact shard, the shards are copied to devices[0] over
+ * the peer link (xGMI) and un-interleaved there.  render_start / render_step
+ * / stop_rendering then drive all devices; the frame is bit-identical to a
+ * one-device render (the RNG is keyed per (pixel, sample)). */
+int pt_renderer_create_multi(pt_scene *scene, const int *devices, int ngpu, uint32_t depth, pt_renderer **out);
+int pt_renderer_num_devices(const pt_renderer *r);
+/* Tuning knobs of the render engines (not part of the reference; defaults are
+ * the measured optimum): "engine" (0 auto, 1 megakernel,
+ * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
+ * "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
+ * "wf_march_blocks_per_cu".  A new renderer takes them from the PT_*
+ * environment variables (PT_ENGINE=mega|wave, PT_WAVES, PT_WF_SLOTS, ...)
+ * once; set_option changes them for every device of the renderer (not while
+ * a render_start frame is in flight).  No knob changes the image: every
+ * setting renders the same bits.  pt_option_name(i) lists the names (NULL
+ * past the end). */
+int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value);
+int pt_renderer_get_option(const pt_renderer *r, const char *name, int64_t *value);
+const char *pt_option_name(int index);
 void pt_renderer_destroy(pt_renderer *r);
 /* Renderer::start_rendering (mod.rs:48-53): queues the whole frame on the
- * GPU and returns at once.  seed keys the per-(pixel, sample) RNG stream. */
+ * GPU(s), in ~8 bands of tile rows, and returns at once.  seed keys the
+ * per-(pixel, sample) RNG stream.  A frame still in flight is stopped first
+ * (the GUI calls stop_rendering before every start, src/bin/main.rs:268). */
 int pt_render_start(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
                     uint32_t samples_number, uint64_t seed);
 /* Renderer::render_step (mod.rs:54): copies every finished band of rows into
@@ -134,13 +162,22 @@ int pt_render_start(pt_renderer *r, const pt_camera *camera, uint32_t width, uin
  * is pending (blocking = 0, step_by_step.rs:101-121 semantics), or blocks
  * until done (blocking = 1, thread_pool_new.rs:96-126 semantics). */
 int pt_render_step(pt_renderer *r, double *rgb, int blocking);
-/* Renderer::stop_rendering (mod.rs:55) */
+/* render_step plus the GUI's display encode (src/bin/main.rs:281-289), done on
+ * the GPU right after each band: rgba (w*h*4 bytes, R G B A per pixel) gets
+ * the encoded rows of every finished band; rgb (may be NULL) the linear ones.
+ * Same return values as pt_render_step. */
+int pt_render_step_rgba8(pt_renderer *r, double *rgb, uint8_t *rgba, int blocking);
+/* Renderer::stop_rendering (mod.rs:55): the frame in flight is abandoned — its
+ * queued kernels see the renderer's stop flag and skip their work — and the
+ * call returns when the device streams are drained.  Bands already copied by
+ * render_step stay valid; the rest of the buffer is not written. */
 int pt_render_stop(pt_renderer *r);
 
 /* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */
 /* Renders this rank's share of the frame straight into device memory on
  * `hip_stream` (a hipStream_t; 0 = the null stream, as in every HIP call and
- * in pt_unshard_device).  Pixels are cut into 16x16 tiles; logical tile k belongs to rank k % world and sits in
+ * in pt_unshard_device), on the renderer's first device.  Pixels are cut into
+ * 16x16 tiles; logical tile k belongs to rank k % world and sits in
  * tile row k / tiles_x at column (k % tiles_x + row) % tiles_x (a diagonal
  * deal, so a rank's columns change from row to row).  world == 1: d_out is
  * the w*h*3 frame.  world > 1: d_out holds this rank's tiles in order,
@@ -148,10 +185,18 @@ int pt_render_stop(pt_renderer *r);
 int pt_render_device(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
                      uint32_t samples_number, uint64_t seed, uint32_t rank, uint32_t world,
                      double *d_out, void *hip_stream);
+/* The whole frame over all of the renderer's devices (pt_renderer_create_multi)
+ * into d_frame (w*h*3 doubles on the first device), ordered after the work
+ * queued on hip_stream (a stream of the first device; 0 = null stream), which
+ * resumes once d_frame holds the frame.  Not while a render_start frame is in
+ * flight (PT_ERR_STATE). */
+int pt_render_frame_device(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                           uint32_t samples_number, uint64_t seed, double *d_frame, void *hip_stream);
 uint32_t pt_shard_tiles(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
 /* Rebuild the frame from `world` gathered shard buffers laid out back to back,
- * each padded to pt_shard_tiles(w, h, 0, world) tiles. */
-int pt_unshard_device(const double *d_gathered, uint32_t width, uint32_t height, uint32_t world,
+ * each padded to pt_shard_tiles(w, h, 0, world) tiles, on HIP device `device`
+ * (-1 = the calling thread's current device) and its stream hip_stream. */
+int pt_unshard_device(int device, const double *d_gathered, uint32_t width, uint32_t height, uint32_t world,
                       double *d_frame, void *hip_stream);
 
 /* ---- probes on the GPU (reference pub fns) ----------------------------- */
@@ -174,19 +219,28 @@ int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *camera, uint32_t wid
  * in order, samples, bounces, sphere/rectangle/cube/marched-shape leaf tests,
  * BVH node slabs, marched-shape box slabs, literal march steps, march jump
  * attempts, march jumps, hits, Lambertian/Metal/Dielectric scatters,
- * rejection-sampling tries, attenuation multiplies.  Used for the FLOP side
+ * rejection-sampling tries, attenuation multiplies, Torus tests, marches
+ * dropped by the march guard.  Used for the FLOP side
  * of the roofline. */
-#define PT_NUM_COUNTERS 18
+#define PT_NUM_COUNTERS 19
 int pt_count_work(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
                   uint32_t samples_number, uint64_t seed, const uint32_t *pixels, size_t n,
                   uint64_t *counters);
 
 /* The RayMarchingShape march alone (src/world/shapes/ray_marching.rs:20-74,
- * Heart) on n object-space jobs of 8 doubles {step, passes, o[3], d[3], 0}:
+ * Heart) on n object-space jobs of 8 doubles {step, passes, o[3], d[3]}:
  * t_out = the march's final t, status = 1 if the passes ended (a hit before
- * the caller's [min_t, max_t] test) else 0, iters = skipping-march iterations.
- * Diagnostic / parity probe. */
+ * the caller's [min_t, max_t] test), 2 if the march guard dropped it, else 0,
+ * iters = skipping-march iterations.  Diagnostic / parity probe. */
 int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters);
+
+/* Marches the guard dropped since the last call (read and cleared), summed over
+ * the renderer's devices.  A march that has not ended after 2^24 skipping
+ * iterations (each >= 1 reference step) is one the reference would not finish
+ * either — e.g. a step below the rounding of t, where t + step == t and
+ * ray_marching.rs:37-51 loops forever; it is taken as a miss (the ray goes on
+ * to the shape's neighbours) and counted here.  Waits for the devices. */
+int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
 
 /* Per-kernel launch timing of the render path (bench / roofline): returns
  * the summed HIP-event durations (ms) and launch counts per kernel kind since
@@ -212,9 +266,18 @@ int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
 int pt_profile_phases(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
                       uint32_t samples_number, uint64_t seed, uint64_t *out);
 
-/* Display encode (src/bin/main.rs:281-289): sqrt -> clamp [0, 0.999] -> *256
- * -> u8, alpha 255; rgba is w*h*4 bytes. Host-side. */
+/* ---- display encode and image output (src/bin/main.rs:71-82, 281-289) -- */
+/* sqrt -> clamp [0, 0.999] -> *256 -> u8 (NaN -> 0), alpha 255; rgba is
+ * npix*4 bytes.  Host-side. */
 int pt_encode_rgba8(const double *rgb, size_t npix, uint8_t *rgba);
+/* The same encode on the GPU: d_rgb / d_rgba in device memory of `device`
+ * (-1 = current), d_rgba 4-byte aligned, queued on hip_stream. */
+int pt_encode_rgba8_device(int device, const double *d_rgb, size_t npix, uint8_t *d_rgba, void *hip_stream);
+/* image::save_buffer(path, rgba, w, h, ColorType::Rgba8) of the GUI's "F"
+ * key: an RGBA8 PNG (stored deflate blocks), or binary PPM (P6, alpha
+ * dropped). */
+int pt_write_png(const char *path, const uint8_t *rgba, uint32_t width, uint32_t height);
+int pt_write_ppm(const char *path, const uint8_t *rgba, uint32_t width, uint32_t height);
 
 /* ---- RNG spec shared with the parity oracle ---------------------------- */
 uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);

@@ -39,9 +39,13 @@ TILE = 16
 EXPORTS = [
     "pt_scene_create_from_json", "pt_scene_destroy", "pt_scene_camera", "pt_scene_num_shapes",
     "pt_scene_get_shape", "pt_scene_num_materials", "pt_scene_get_material", "pt_camera_new",
-    "pt_renderer_create", "pt_renderer_destroy", "pt_render_start", "pt_render_step", "pt_render_stop",
-    "pt_render_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit", "pt_ray_color",
-    "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_wave_diag", "pt_kernel_timing", "pt_encode_rgba8", "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_renderer_create", "pt_renderer_create_multi", "pt_renderer_num_devices", "pt_renderer_destroy",
+    "pt_renderer_set_option", "pt_renderer_get_option", "pt_option_name",
+    "pt_render_start", "pt_render_step", "pt_render_step_rgba8", "pt_render_stop",
+    "pt_render_device", "pt_render_frame_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit",
+    "pt_ray_color", "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_march_guard_drops", "pt_wave_diag",
+    "pt_kernel_timing", "pt_encode_rgba8", "pt_encode_rgba8_device", "pt_write_png", "pt_write_ppm",
+    "pt_sample_key", "pt_last_error", "pt_version",
 ]
 
 
@@ -125,13 +129,20 @@ def lib():
         "pt_scene_get_material": (C.c_int, [vp, C.c_int, C.POINTER(MaterialInfo)]),
         "pt_camera_new": (C.c_int, [d, d, d, C.c_double, C.c_double, C.POINTER(CameraStruct)]),
         "pt_renderer_create": (C.c_int, [vp, C.c_int, u32, C.POINTER(vp)]),
+        "pt_renderer_create_multi": (C.c_int, [vp, C.POINTER(C.c_int), C.c_int, u32, C.POINTER(vp)]),
+        "pt_renderer_num_devices": (C.c_int, [vp]),
+        "pt_renderer_set_option": (C.c_int, [vp, C.c_char_p, C.c_int64]),
+        "pt_renderer_get_option": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int64)]),
+        "pt_option_name": (C.c_char_p, [C.c_int]),
         "pt_renderer_destroy": (None, [vp]),
         "pt_render_start": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64]),
         "pt_render_step": (C.c_int, [vp, d, C.c_int]),
+        "pt_render_step_rgba8": (C.c_int, [vp, d, C.POINTER(C.c_uint8), C.c_int]),
         "pt_render_stop": (C.c_int, [vp]),
         "pt_render_device": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, u32, u32, vp, vp]),
+        "pt_render_frame_device": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, vp, vp]),
         "pt_shard_tiles": (u32, [u32, u32, u32, u32]),
-        "pt_unshard_device": (C.c_int, [vp, u32, u32, u32, vp, vp]),
+        "pt_unshard_device": (C.c_int, [C.c_int, vp, u32, u32, u32, vp, vp]),
         "pt_closest_hit": (C.c_int, [vp, d, sz, C.c_double, C.c_double, vp]),
         "pt_ray_color": (C.c_int, [vp, d, C.POINTER(u64), sz, u32, d]),
         "pt_trace_pixel_samples": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64,
@@ -141,9 +152,13 @@ def lib():
         "pt_march_jobs": (C.c_int, [vp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), C.POINTER(C.c_int32),
                                     C.POINTER(C.c_uint32)]),
         "pt_kernel_timing": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(u32), sz]),
+        "pt_march_guard_drops": (C.c_int, [vp, C.POINTER(u64)]),
         "pt_wave_diag": (C.c_int, [vp, C.c_int, C.POINTER(u64), sz]),
         "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
+        "pt_encode_rgba8_device": (C.c_int, [C.c_int, vp, sz, vp, vp]),
+        "pt_write_png": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), u32, u32]),
+        "pt_write_ppm": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), u32, u32]),
         "pt_sample_key": (u64, [u64, u64, u64]),
         "pt_last_error": (C.c_char_p, []),
         "pt_version": (C.c_char_p, []),
@@ -279,18 +294,41 @@ class Renderer(abc.ABC):
 
 class HipRenderer(Renderer):
     """The MI355X renderer: ThreadPoolRenderer::new(scene, thread_number, depth)
-    with a HIP device in place of the thread pool.  `seed` keys the per-(pixel,
-    sample) RNG; render_step(blocking=False) is step_by_step's non-blocking
-    drain, blocking=True is thread_pool_new's."""
+    with HIP devices in place of the thread pool.  `device` is one HIP ordinal
+    (-1 = current); `devices` (a list of ordinals, may repeat) spreads the
+    frame's tiles over several (pt_renderer_create_multi).  `seed` keys the
+    per-(pixel, sample) RNG; render_step(blocking=False) is step_by_step's
+    non-blocking drain, blocking=True is thread_pool_new's."""
 
-    def __init__(self, scene: Scene, device: int = -1, depth: int = 50, seed: int = 1):
+    def __init__(self, scene: Scene, device: int = -1, depth: int = 50, seed: int = 1, devices=None):
         self.scene = scene  # must outlive the renderer
         self.depth = int(depth)
         self.seed = int(seed)
         h = C.c_void_p()
-        _check(lib().pt_renderer_create(scene._h, int(device), self.depth, C.byref(h)))
+        if devices is None:
+            _check(lib().pt_renderer_create(scene._h, int(device), self.depth, C.byref(h)))
+        else:
+            dv = (C.c_int * len(devices))(*[int(x) for x in devices])
+            _check(lib().pt_renderer_create_multi(scene._h, dv, len(devices), self.depth, C.byref(h)))
         self._h = h
         self._shape = None
+
+    @property
+    def num_devices(self) -> int:
+        return _check(lib().pt_renderer_num_devices(self._h))
+
+    def set_option(self, name: str, value: int):
+        """A tuning knob (pt_renderer_set_option): "engine" 0 auto / 1 megakernel / 2 wavefront, "wf_slots", ..."""
+        _check(lib().pt_renderer_set_option(self._h, name.encode(), int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        _check(lib().pt_renderer_get_option(self._h, name.encode(), C.byref(v)))
+        return v.value
+
+    def options(self) -> dict:
+        """Every tuning knob and its current value."""
+        return {n: self.get_option(n) for n in option_names()}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -311,6 +349,21 @@ class HipRenderer(Renderer):
             raise ValueError("buffer must be a C-contiguous float64 array of shape %r" % (self._shape,))
         return _check(lib().pt_render_step(self._h, _dptr(buffer), 1 if blocking else 0)) == 1
 
+    def render_step_rgba8(self, rgba: np.ndarray, buffer: np.ndarray | None = None, blocking: bool = False) -> bool:
+        """render_step with the GPU's display encode of every finished band in
+        rgba ((w*h, 4) uint8); buffer (optional) gets the linear rows too."""
+        if self._shape is None:
+            raise PtError(PT_ERR_STATE, "render_step before start_rendering")
+        if rgba.shape != (self._shape[0], 4) or rgba.dtype != np.uint8 or not rgba.flags.c_contiguous:
+            raise ValueError("rgba must be a C-contiguous uint8 array of shape (%d, 4)" % self._shape[0])
+        bp = None
+        if buffer is not None:
+            if buffer.shape != self._shape or buffer.dtype != np.float64 or not buffer.flags.c_contiguous:
+                raise ValueError("buffer must be a C-contiguous float64 array of shape %r" % (self._shape,))
+            bp = _dptr(buffer)
+        return _check(lib().pt_render_step_rgba8(self._h, bp, rgba.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                 1 if blocking else 0)) == 1
+
     def stop_rendering(self):
         _check(lib().pt_render_stop(self._h))
 
@@ -326,6 +379,13 @@ class HipRenderer(Renderer):
         (0 = the null stream; see pt_render_device)."""
         _check(lib().pt_render_device(self._h, C.byref(camera._c), width, height, spp, seed, rank, world,
                                       C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
+
+    def render_frame_device(self, camera: Camera, width: int, height: int, spp: int, seed: int, frame_ptr: int,
+                            stream_ptr: int = 0):
+        """The whole frame over all of the renderer's devices into device memory at frame_ptr (first
+        device), ordered after stream_ptr's queued work (pt_render_frame_device)."""
+        _check(lib().pt_render_frame_device(self._h, C.byref(camera._c), width, height, spp, seed,
+                                            C.c_void_p(frame_ptr), C.c_void_p(stream_ptr)))
 
     # ---- probes --------------------------------------------------------
     def closest_hit(self, rays: np.ndarray, min_t: float = 0.001, max_t: float = float("inf")) -> np.ndarray:
@@ -357,7 +417,7 @@ class HipRenderer(Renderer):
 
 COUNTERS = ["samples", "bounces", "test_sphere", "test_rect", "test_cube", "test_march", "node_slabs",
             "march_slabs", "march_steps", "march_tries", "march_blocks", "hits", "lambert", "metal",
-            "dielectric", "reject_tries", "unwind", "test_torus"]
+            "dielectric", "reject_tries", "unwind", "test_torus", "march_guard"]
 
 
 def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams, samples_number: int,
@@ -372,9 +432,17 @@ def count_work(renderer: "HipRenderer", camera: Camera, img_params: ImageParams,
     return dict(zip(COUNTERS, list(out)))
 
 
-def march_jobs(renderer: "HipRenderer", jobs):
+def march_guard_drops(renderer: "HipRenderer") -> int:
+    """Marches dropped by the 2^24-iteration guard since the last call (pt_march_guard_drops)."""
+    n = C.c_uint64()
+    _check(lib().pt_march_guard_drops(renderer._h, C.byref(n)))
+    return n.value
+
+
+def march_jobs(renderer: "HipRenderer", jobs, status=False):
     """The skipping Heart march alone on the GPU (pt_march_jobs): jobs is an
-    (n, 8) float64 array {step, passes, o, d, 0}; returns (t, hit, iters)."""
+    (n, 8) float64 array {step, passes, o, d}; returns (t, hit, iters), or
+    (t, status, iters) with status 1 hit / 0 miss / 2 dropped by the guard."""
     import numpy as np
     jobs = np.ascontiguousarray(jobs, dtype=np.float64).reshape(-1, 8)
     n = len(jobs)
@@ -384,7 +452,7 @@ def march_jobs(renderer: "HipRenderer", jobs):
     dp = C.POINTER(C.c_double)
     _check(lib().pt_march_jobs(renderer._h, jobs.ctypes.data_as(dp), n, t.ctypes.data_as(dp),
                                st.ctypes.data_as(C.POINTER(C.c_int32)), it.ctypes.data_as(C.POINTER(C.c_uint32))))
-    return t, st.astype(bool), it
+    return (t, st, it) if status else (t, st == 1, it)
 
 
 KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel"]
@@ -415,6 +483,22 @@ def profile_phases(renderer: "HipRenderer", camera: Camera, img_params: ImagePar
                                    int(samples_number), s, out))
     return dict(zip(["trace", "march", "select", "shade", "passes", "march_passes", "max_passes",
                     "shade_finish", "shade_scatter", "shade_restart"], list(out)))
+
+
+def option_names() -> list:
+    out, i = [], 0
+    while True:
+        n = lib().pt_option_name(i)
+        if n is None:
+            return out
+        out.append(n.decode())
+        i += 1
+
+
+# the defaults (pt_kernel.hpp Tuning): bench.py reports knobs that differ
+OPTION_DEFAULTS = {"engine": 0, "mega_waves": 4, "diag": 0, "wf_slots": 2, "wf_paths": 1 << 24, "wf_min_chunks": 1,
+                   "wf_bounce_waves": 3, "wf_fused": 0, "wf_march_slice": 256, "wf_trace_slice": 256,
+                   "wf_march_blocks_per_cu": 0}
 
 
 def shard_tiles(width: int, height: int, rank: int, world: int) -> int:
@@ -450,9 +534,10 @@ def unshard_host(gathered: np.ndarray, width: int, height: int, world: int) -> n
     return frame
 
 
-def unshard_device(gathered_ptr: int, width: int, height: int, world: int, frame_ptr: int, stream_ptr: int = 0):
-    _check(lib().pt_unshard_device(C.c_void_p(gathered_ptr), width, height, world, C.c_void_p(frame_ptr),
-                                   C.c_void_p(stream_ptr)))
+def unshard_device(gathered_ptr: int, width: int, height: int, world: int, frame_ptr: int, stream_ptr: int = 0,
+                   device: int = -1):
+    _check(lib().pt_unshard_device(int(device), C.c_void_p(gathered_ptr), width, height, world,
+                                   C.c_void_p(frame_ptr), C.c_void_p(stream_ptr)))
 
 
 def encode_rgba8(buffer: np.ndarray) -> np.ndarray:
@@ -461,6 +546,30 @@ def encode_rgba8(buffer: np.ndarray) -> np.ndarray:
     out = np.zeros((len(buf), 4), dtype=np.uint8)
     _check(lib().pt_encode_rgba8(_dptr(buf), len(buf), out.ctypes.data_as(C.POINTER(C.c_uint8))))
     return out
+
+
+def encode_rgba8_device(rgb_ptr: int, npix: int, rgba_ptr: int, stream_ptr: int = 0, device: int = -1):
+    """The display encode on the GPU (pt_encode_rgba8_device): device pointers."""
+    _check(lib().pt_encode_rgba8_device(int(device), C.c_void_p(rgb_ptr), int(npix), C.c_void_p(rgba_ptr),
+                                        C.c_void_p(stream_ptr)))
+
+
+def _image_args(rgba: np.ndarray, width: int, height: int):
+    rgba = np.ascontiguousarray(rgba, dtype=np.uint8).reshape(-1)
+    if rgba.size != width * height * 4:
+        raise ValueError("rgba must hold width*height*4 bytes")
+    return rgba, rgba.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def write_png(path, rgba: np.ndarray, width: int, height: int):
+    """image::save_buffer(path, rgba, w, h, ColorType::Rgba8) (src/bin/main.rs:71-82)."""
+    buf, p = _image_args(rgba, width, height)
+    _check(lib().pt_write_png(str(path).encode(), p, width, height))
+
+
+def write_ppm(path, rgba: np.ndarray, width: int, height: int):
+    buf, p = _image_args(rgba, width, height)
+    _check(lib().pt_write_ppm(str(path).encode(), p, width, height))
 
 
 def sample_key(seed: int, pixel: int, sample: int) -> int:

@@ -6,10 +6,13 @@
 // frame is still on the GPU (src/renderer/step_by_step.rs:101-121).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -56,31 +59,61 @@ struct pt_scene {
     Scene s;
 };
 
-struct pt_renderer {
-    pt_scene *scene = nullptr;
+// One device of a renderer: its own copy of the scene, wavefront workspace
+// and stream.  A single-device renderer has one; a multi-device
+// renderer (pt_renderer_create_multi) deals the frame's tiles to several,
+// rank g = gpus[g], and gathers the shards on gpus[0].
+struct GpuShare {
     int device = 0;
-    uint32_t depth = 0;
     hipStream_t stream = nullptr;
     DeviceScene ds;
-    WaveWorkspace ws;  // wavefront engine state (scenes with ray-marched shapes)
-    double s11 = 0;
+    WaveWorkspace ws;
+    double *d_shard = nullptr;  // compact tile shard of a multi-device frame (ranks >= 1)
+    size_t shard_cap = 0;
+    hipEvent_t shard_ev = nullptr;  // a band's shard copy to gpus[0] is done
+};
 
-    // frame in flight
+struct pt_renderer {
+    pt_scene *scene = nullptr;
+    uint32_t depth = 0;
+    double s11 = 0;
+    std::vector<GpuShare> gpus;  // gpus[0] holds the frame
+
+    // frame in flight (render_start .. render_step)
     bool started = false;
     uint32_t width = 0, height = 0;
-    double *d_frame = nullptr;
+    double *d_frame = nullptr;  // w*h*3 on gpus[0]
     size_t frame_cap = 0;
+    uint8_t *d_rgba = nullptr;  // w*h*4 display encode of d_frame, on gpus[0]
+    size_t rgba_cap = 0;
+    double *d_gather = nullptr;  // multi-device: world shards back to back, on gpus[0]
+    size_t gather_cap = 0;
+    // A progressive frame is a list of bands of tile rows.  A feeder thread
+    // queues them on the device(s), keeping two bands ahead of the GPU (one
+    // running, one queued), so the device never idles between bands and
+    // stop_rendering only has to drain at most two of them.
     struct Band {
-        uint32_t row0, row1;
-        hipEvent_t ev;
+        uint32_t t0, t1;      // tile rows
+        uint32_t row0, row1;  // pixel rows
+        hipEvent_t ev;        // recorded on gpus[0].stream once the band is queued
         bool copied;
     };
     std::vector<Band> bands;
+    FrameParams frame{};
+    std::thread feeder;
+    std::atomic<bool> stop_req{false};
+    std::atomic<uint32_t> bands_queued{0};  // bands [0, n) are queued (their events recorded)
+    std::atomic<int> feed_rc{0};            // the feeder's failure status (feed_err holds the message)
+    std::string feed_err;
+
+    int device() const { return gpus[0].device; }
+    hipStream_t stream() const { return gpus[0].stream; }
 };
 
 extern "C" {
 
 const char *pt_last_error(void) { return g_err.c_str(); }
+__attribute__((visibility("hidden"))) void pt_set_last_error(const char *msg) { g_err = msg ? msg : ""; }  // for pt_image.cpp
 const char *pt_version(void) { return "rs-pathtracing-amd 0.2.0 (gfx950, f64 megakernel + wavefront march engine)"; }
 
 uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample) { return sample_key(seed, pixel, sample); }
@@ -174,29 +207,35 @@ int pt_camera_new(const double position[3], const double direction[3], const dou
 }
 
 // ------------------------------------------------------------- renderer
-int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer **out) {
-    if (!scene || !out) return fail(PT_ERR_INVALID, "null argument");
-    *out = nullptr;
-    if (depth > 64) return fail(PT_ERR_UNSUPPORTED, "depth > 64 is not supported on the GPU path");
-    int count = 0;
-    hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess || count == 0) return fail(PT_ERR_HIP, "no HIP device available (the GPU path has no CPU fallback)");
-    if (device < 0) HIP_TRY(hipGetDevice(&device));
-    if (device >= count) return fail(PT_ERR_INVALID, "device ordinal out of range");
+}  // extern "C"
+
+namespace {
+
+void free_share(GpuShare &g) {
+    (void)hipSetDevice(g.device);
+    if (g.stream) (void)hipStreamSynchronize(g.stream);
+    DeviceScene &d = g.ds;
+    void *bufs[] = {d.shapes, d.mats, d.nodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images, d.pixels,
+                    d.guard};
+    for (void *p : bufs)
+        if (p) (void)hipFree(p);
+    d = DeviceScene{};
+    if (g.d_shard) (void)hipFree(g.d_shard);
+    g.d_shard = nullptr;
+    g.shard_cap = 0;
+    wave_workspace_free(&g.ws);
+    if (g.shard_ev) (void)hipEventDestroy(g.shard_ev);
+    g.shard_ev = nullptr;
+    if (g.stream) (void)hipStreamDestroy(g.stream);
+    g.stream = nullptr;
+}
+
+// Uploads the realized scene to one device and creates its stream and stop flag.
+int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const std::vector<DShape> &hs,
+               const std::vector<DMaterial> &hm) {
+    g.device = device;
     HIP_TRY(hipSetDevice(device));
-    pt_renderer *r = new (std::nothrow) pt_renderer;
-    if (!r) return fail(PT_ERR_INVALID, "out of memory");
-    r->scene = scene;
-    r->device = device;
-    r->depth = depth;
-    r->s11 = uniform_incl_scale(-1.0, 1.0);
-    std::vector<DShape> hs;
-    std::vector<DMaterial> hm;
-    for (auto &s : scene->s.shapes) hs.push_back(to_device(s));
-    for (auto &m : scene->s.materials) hm.push_back(to_device(m));
-    if (hm.empty()) hm.push_back(DMaterial{});
-    Accel acc = build_accel(scene->s, scene->s.json_shapes);
-    hipError_t err = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+    hipError_t err = hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking);
     auto upload = [&err](auto **dst, const auto &vec) {
         using T = typename std::remove_reference<decltype(vec)>::type::value_type;
         size_t n = vec.empty() ? 1 : vec.size();
@@ -204,69 +243,54 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
         if (err == hipSuccess && !vec.empty())
             err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice);
     };
-    upload(&r->ds.shapes, hs);
-    upload(&r->ds.mats, hm);
-    upload(&r->ds.nodes, acc.cnodes);
-    upload(&r->ds.leaf, acc.leaf);
-    upload(&r->ds.lin, acc.lin);
-    upload(&r->ds.march, acc.march);
-    upload(&r->ds.boxes, acc.boxes);
-    const Scene &S = scene->s;
+    upload(&g.ds.shapes, hs);
+    upload(&g.ds.mats, hm);
+    upload(&g.ds.nodes, acc.cnodes);
+    upload(&g.ds.leaf, acc.leaf);
+    upload(&g.ds.lin, acc.lin);
+    upload(&g.ds.march, acc.march);
+    upload(&g.ds.boxes, acc.boxes);
     if (!S.textures.empty()) {
-        upload(&r->ds.tex, S.textures);
-        upload(&r->ds.perlin, S.perlins);
-        upload(&r->ds.images, S.images);
-        upload(&r->ds.pixels, S.pixels);
+        upload(&g.ds.tex, S.textures);
+        upload(&g.ds.perlin, S.perlins);
+        upload(&g.ds.images, S.images);
+        upload(&g.ds.pixels, S.pixels);
     }
-    if (err != hipSuccess) {
-        pt_renderer_destroy(r);
-        return hip_fail(err, "uploading the scene");
-    }
-    r->ds.nshapes = (int)hs.size();
-    r->ds.nmats = (int)hm.size();
-    r->ds.nnodes = acc.nodes_per_octant();  // nodes per octant layout
-    r->ds.nlin = (int)acc.lin.size();
-    r->ds.nmarch = (int)acc.march.size();
-    r->ds.ext = S.textures.empty() ? 0 : 1;
+    if (err == hipSuccess) err = hipEventCreateWithFlags(&g.shard_ev, hipEventDisableTiming);
+    if (err == hipSuccess) err = hipMalloc((void **)&g.ds.guard, sizeof(unsigned long long));
+    if (err == hipSuccess) err = hipMemset(g.ds.guard, 0, sizeof(unsigned long long));
+    if (err != hipSuccess) return hip_fail(err, "uploading the scene");
+    g.ws.tune = tuning_from_env();
+    g.ds.diag = g.ws.tune.diag;
+    g.ds.nshapes = (int)hs.size();
+    g.ds.nmats = (int)hm.size();
+    g.ds.nnodes = acc.nodes_per_octant();  // nodes per octant layout
+    g.ds.nlin = (int)acc.lin.size();
+    g.ds.nmarch = (int)acc.march.size();
+    g.ds.ext = S.textures.empty() ? 0 : 1;
     for (const auto &h : S.shapes)
-        if (h.type == TORUS) r->ds.ext = 1;
-    r->ds.fkind = 0;  // Heart-only kernel builds unless another function is marched
-    for (const auto &h : r->scene->s.shapes)
-        if (h.type == MARCH && h.func != 0) r->ds.fkind = -1;
-    *out = r;
+        if (h.type == TORUS) g.ds.ext = 1;
+    g.ds.fkind = 0;  // Heart-only kernel builds unless another function is marched
+    for (const auto &h : S.shapes)
+        if (h.type == MARCH && h.func != 0) g.ds.fkind = -1;
     return PT_OK;
 }
 
-static void release_bands(pt_renderer *r) {
+void release_bands(pt_renderer *r) {
     for (auto &b : r->bands) (void)hipEventDestroy(b.ev);
     r->bands.clear();
 }
 
-void pt_renderer_destroy(pt_renderer *r) {
-    if (!r) return;
-    (void)hipSetDevice(r->device);
-    if (r->stream) (void)hipStreamSynchronize(r->stream);
-    release_bands(r);
-    if (r->d_frame) (void)hipFree(r->d_frame);
-    if (r->ds.shapes) (void)hipFree(r->ds.shapes);
-    if (r->ds.mats) (void)hipFree(r->ds.mats);
-    if (r->ds.nodes) (void)hipFree(r->ds.nodes);
-    if (r->ds.leaf) (void)hipFree(r->ds.leaf);
-    if (r->ds.lin) (void)hipFree(r->ds.lin);
-    if (r->ds.march) (void)hipFree(r->ds.march);
-    if (r->ds.boxes) (void)hipFree(r->ds.boxes);
-    if (r->ds.tex) (void)hipFree(r->ds.tex);
-    if (r->ds.perlin) (void)hipFree(r->ds.perlin);
-    if (r->ds.images) (void)hipFree(r->ds.images);
-    if (r->ds.pixels) (void)hipFree(r->ds.pixels);
-    if (r->stream) (void)hipStreamSynchronize(r->stream);
-    wave_workspace_free(&r->ws);
-    if (r->stream) (void)hipStreamDestroy(r->stream);
-    delete r;
+int sync_all(pt_renderer *r) {
+    for (auto &g : r->gpus) {
+        HIP_TRY(hipSetDevice(g.device));
+        HIP_TRY(hipStreamSynchronize(g.stream));
+    }
+    return PT_OK;
 }
 
-static FrameParams frame_params(const pt_renderer *r, const pt_camera &cam, uint32_t w, uint32_t h, uint32_t spp,
-                                uint64_t seed) {
+FrameParams frame_params(const pt_renderer *r, const pt_camera &cam, uint32_t w, uint32_t h, uint32_t spp,
+                         uint64_t seed) {
     FrameParams P;
     std::memset(&P, 0, sizeof P);
     caster_params(cam, w, h, &P);
@@ -282,51 +306,298 @@ static FrameParams frame_params(const pt_renderer *r, const pt_camera &cam, uint
     return P;
 }
 
+// The part [*i0, *i1) of rank's tile list whose logical tiles lie in [a, b):
+// logical tile k belongs to rank k % world at list index k / world.
+void rank_range(uint32_t a, uint32_t b, uint32_t rank, uint32_t world, uint32_t *i0, uint32_t *i1) {
+    *i0 = a > rank ? (a - rank + world - 1) / world : 0;
+    *i1 = b > rank ? (b - rank + world - 1) / world : 0;
+}
+
+template <class T>
+int grow(T **p, size_t *cap, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes <= *cap) return PT_OK;
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc((void **)p, bytes));
+    *cap = bytes;
+    return PT_OK;
+}
+
+// Buffers of a frame on the renderer's devices (world > 1: the shards and the
+// gather buffer), and the fork: the other devices' streams start after
+// everything queued so far on gpus[0]'s stream.
+int frame_prologue(pt_renderer *r, uint32_t w, uint32_t h) {
+    const uint32_t world = (uint32_t)r->gpus.size();
+    if (world == 1) return PT_OK;
+    GpuShare &g0 = r->gpus[0];
+    const size_t per = pt_shard_tiles(w, h, 0, world);
+    HIP_TRY(hipSetDevice(g0.device));
+    if (int rc = grow(&r->d_gather, &r->gather_cap, (size_t)world * per * TILE * TILE * 3)) return rc;
+    HIP_TRY(hipEventRecord(g0.shard_ev, g0.stream));
+    for (uint32_t k = 1; k < world; k++) {
+        GpuShare &g = r->gpus[k];
+        HIP_TRY(hipSetDevice(g.device));
+        if (int rc = grow(&g.d_shard, &g.shard_cap, per * TILE * TILE * 3)) return rc;
+        HIP_TRY(hipStreamWaitEvent(g.stream, g0.shard_ev, 0));
+    }
+    return PT_OK;
+}
+
+// Queues tile rows [t0, t1) of the frame: every device renders its tiles of
+// the band (world > 1: into its compact shard, then copied to gpus[0] over
+// the peer link), gpus[0] un-interleaves the band into d_frame, encodes it
+// into d_rgba (if given) and records `ev` (if given).
+int enqueue_band(pt_renderer *r, const FrameParams &P0, double *d_frame, uint8_t *d_rgba, uint32_t t0, uint32_t t1,
+                 hipEvent_t ev) {
+    const uint32_t world = (uint32_t)r->gpus.size();
+    const uint32_t w = P0.width, h = P0.height, tx = P0.tiles_x;
+    GpuShare &g0 = r->gpus[0];
+    const size_t per = pt_shard_tiles(w, h, 0, world);
+    const uint32_t row0 = t0 * TILE, row1 = t1 * TILE < h ? t1 * TILE : h;
+    for (uint32_t k = 0; k < world; k++) {
+        GpuShare &g = r->gpus[k];
+        HIP_TRY(hipSetDevice(g.device));
+        FrameParams P = P0;
+        P.rank = k;
+        P.world = world;
+        P.compact = world > 1 ? 1 : 0;
+        uint32_t i0, i1;
+        rank_range(t0 * tx, t1 * tx, k, world, &i0, &i1);
+        P.tile_begin = i0;
+        P.tile_count = i1 - i0;
+        double *dst = world == 1 ? d_frame : (k == 0 ? r->d_gather : g.d_shard);
+        HIP_TRY(launch_render(g.ds, P, dst, g.stream, &g.ws));
+        if (k > 0) {
+            if (i1 > i0) {
+                const size_t off = (size_t)i0 * TILE * TILE * 3, n = (size_t)(i1 - i0) * TILE * TILE * 3;
+                HIP_TRY(hipMemcpyPeerAsync(r->d_gather + (size_t)k * per * TILE * TILE * 3 + off, g0.device,
+                                           g.d_shard + off, g.device, n * sizeof(double), g.stream));
+            }
+            HIP_TRY(hipEventRecord(g.shard_ev, g.stream));
+            HIP_TRY(hipSetDevice(g0.device));
+            HIP_TRY(hipStreamWaitEvent(g0.stream, g.shard_ev, 0));
+        }
+    }
+    HIP_TRY(hipSetDevice(g0.device));
+    if (world > 1) HIP_TRY(launch_unshard(r->d_gather, w, h, world, d_frame, g0.stream, row0, row1));
+    if (d_rgba) HIP_TRY(launch_encode_rgba8(d_frame, (size_t)row0 * w, (size_t)row1 * w, d_rgba, g0.stream));
+    if (ev) HIP_TRY(hipEventRecord(ev, g0.stream));
+    return PT_OK;
+}
+
+// The feeder thread of a progressive frame: queues band b once band b - 2 is
+// done, until the frame is queued or stop_rendering asks it to stop.
+void feed_bands(pt_renderer *r) {
+    const size_t n = r->bands.size();
+    for (size_t b = 0; b < n; b++) {
+        if (r->stop_req.load()) return;
+        if (b >= 2) {
+            (void)hipSetDevice(r->device());
+            hipError_t e = hipEventSynchronize(r->bands[b - 2].ev);
+            if (e != hipSuccess) {
+                r->feed_err = std::string("hipEventSynchronize: ") + hipGetErrorString(e);
+                r->feed_rc.store(PT_ERR_HIP);
+                return;
+            }
+            if (r->stop_req.load()) return;
+        }
+        const auto &B = r->bands[b];
+        if (int rc = enqueue_band(r, r->frame, r->d_frame, r->d_rgba, B.t0, B.t1, B.ev)) {
+            r->feed_err = g_err;  // this thread's message
+            r->feed_rc.store(rc);
+            return;
+        }
+        r->bands_queued.store((uint32_t)(b + 1));
+    }
+}
+
+void join_feeder(pt_renderer *r) {
+    if (r->feeder.joinable()) r->feeder.join();
+}
+
+int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t depth, pt_renderer **out) {
+    *out = nullptr;
+    if (depth > 64) return fail(PT_ERR_UNSUPPORTED, "depth > 64 is not supported on the GPU path");
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) return fail(PT_ERR_HIP, "no HIP device available (the GPU path has no CPU fallback)");
+    for (int d : devices)
+        if (d < 0 || d >= count) return fail(PT_ERR_INVALID, "device ordinal out of range");
+    pt_renderer *r = new (std::nothrow) pt_renderer;
+    if (!r) return fail(PT_ERR_INVALID, "out of memory");
+    r->scene = scene;
+    r->depth = depth;
+    r->s11 = uniform_incl_scale(-1.0, 1.0);
+    try {
+        std::vector<DShape> hs;
+        std::vector<DMaterial> hm;
+        for (auto &s : scene->s.shapes) hs.push_back(to_device(s));
+        for (auto &m : scene->s.materials) hm.push_back(to_device(m));
+        if (hm.empty()) hm.push_back(DMaterial{});
+        const Accel acc = build_accel(scene->s, scene->s.json_shapes);
+        r->gpus.resize(devices.size());
+        for (size_t k = 0; k < devices.size(); k++) {
+            if (int rc = init_share(r->gpus[k], devices[k], scene->s, acc, hs, hm)) {
+                pt_renderer_destroy(r);
+                return rc;
+            }
+        }
+    } catch (const std::bad_alloc &) {
+        pt_renderer_destroy(r);
+        return fail(PT_ERR_INVALID, "out of memory");
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = r;
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer **out) {
+    if (!scene || !out) return fail(PT_ERR_INVALID, "null argument");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(PT_ERR_HIP, "no HIP device available (the GPU path has no CPU fallback)");
+    if (device < 0) HIP_TRY(hipGetDevice(&device));
+    return create_renderer(scene, {device}, depth, out);
+}
+
+int pt_renderer_create_multi(pt_scene *scene, const int *devices, int ngpu, uint32_t depth, pt_renderer **out) {
+    if (!scene || !out) return fail(PT_ERR_INVALID, "null argument");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(PT_ERR_HIP, "no HIP device available (the GPU path has no CPU fallback)");
+    if (ngpu <= 0) {
+        if (devices) return fail(PT_ERR_INVALID, "ngpu must be > 0 when devices are listed");
+        ngpu = count;
+    }
+    std::vector<int> dv((size_t)ngpu);
+    for (int k = 0; k < ngpu; k++) dv[k] = devices ? devices[k] : k;
+    return create_renderer(scene, dv, depth, out);
+}
+
+int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
+    if (!r || !name) return fail(PT_ERR_INVALID, "null argument");
+    if (r->started) return fail(PT_ERR_STATE, "options cannot change while a frame is in flight");
+    for (auto &g : r->gpus) {
+        Tuning t = g.ws.tune;
+        if (tuning_set(&t, name, value) != PT_OK)
+            return fail(PT_ERR_INVALID, std::string("unknown option or value out of range: ") + name + " = " +
+                                            std::to_string((long long)value));
+        // the workspace may be in use by a frame queued on any stream
+        HIP_TRY(hipSetDevice(g.device));
+        HIP_TRY(hipDeviceSynchronize());
+        g.ws.tune = t;
+        g.ds.diag = t.diag;
+    }
+    return PT_OK;
+}
+
+int pt_renderer_get_option(const pt_renderer *r, const char *name, int64_t *value) {
+    if (!r || !name || !value) return fail(PT_ERR_INVALID, "null argument");
+    if (tuning_get(r->gpus[0].ws.tune, name, value) != PT_OK) return fail(PT_ERR_INVALID, std::string("unknown option: ") + name);
+    return PT_OK;
+}
+
+const char *pt_option_name(int index) {
+    int n = 0;
+    while (TUNING_NAMES[n]) n++;
+    return index >= 0 && index < n ? TUNING_NAMES[index] : nullptr;
+}
+
+int pt_renderer_num_devices(const pt_renderer *r) { return r ? (int)r->gpus.size() : fail(PT_ERR_INVALID, "null renderer"); }
+
+void pt_renderer_destroy(pt_renderer *r) {
+    if (!r) return;
+    if (r->started) (void)pt_render_stop(r);
+    join_feeder(r);
+    (void)sync_all(r);
+    release_bands(r);
+    if (!r->gpus.empty()) {
+        (void)hipSetDevice(r->device());
+        if (r->d_frame) (void)hipFree(r->d_frame);
+        if (r->d_rgba) (void)hipFree(r->d_rgba);
+        if (r->d_gather) (void)hipFree(r->d_gather);
+    }
+    for (auto &g : r->gpus) free_share(g);
+    delete r;
+}
+
 int pt_render_start(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed) {
     if (!r || !cam) return fail(PT_ERR_INVALID, "null argument");
     if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
-    HIP_TRY(hipSetDevice(r->device));
-    if (r->started) {  // a new frame replaces the one in flight
-        HIP_TRY(hipStreamSynchronize(r->stream));
-        release_bands(r);
+    if (r->started) {  // a new frame replaces the one in flight (the reference stops it first, main.rs:268)
+        if (int rc = pt_render_stop(r)) return rc;
     }
-    size_t bytes = (size_t)w * h * 3 * sizeof(double);
-    if (bytes > r->frame_cap) {
-        if (r->d_frame) HIP_TRY(hipFree(r->d_frame));
-        r->d_frame = nullptr;
-        r->frame_cap = 0;
-        HIP_TRY(hipMalloc(&r->d_frame, bytes));
-        r->frame_cap = bytes;
-    }
-    FrameParams P = frame_params(r, *cam, w, h, spp, seed);
-    uint32_t ty = tiles_y_of(h);
-    uint32_t band = ty >= 8 ? ty / 8 : 1;  // ~8 progressive bands per frame
+    HIP_TRY(hipSetDevice(r->device()));
+    if (int rc = grow(&r->d_frame, &r->frame_cap, (size_t)w * h * 3)) return rc;
+    if (int rc = grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4)) return rc;
+    if (int rc = frame_prologue(r, w, h)) return rc;
+    r->frame = frame_params(r, *cam, w, h, spp, seed);
+    // ~8 bands of whole tile rows: a band is one pass of the engine over
+    // 1/8 of the frame, big enough to fill the device
+    const uint32_t ty = tiles_y_of(h);
+    const uint32_t band = ty >= 8 ? ty / 8 : 1;
+    release_bands(r);
     for (uint32_t t0 = 0; t0 < ty; t0 += band) {
-        uint32_t t1 = t0 + band < ty ? t0 + band : ty;
-        P.tile_begin = t0 * P.tiles_x;
-        P.tile_count = (t1 - t0) * P.tiles_x;
-        HIP_TRY(launch_render(r->ds, P, r->d_frame, r->stream, &r->ws));
         pt_renderer::Band b;
+        b.t0 = t0;
+        b.t1 = t0 + band < ty ? t0 + band : ty;
         b.row0 = t0 * TILE;
-        b.row1 = t1 * TILE < h ? t1 * TILE : h;
+        b.row1 = b.t1 * TILE < h ? b.t1 * TILE : h;
         b.copied = false;
-        HIP_TRY(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(b.ev, r->stream));
+        hipError_t e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            release_bands(r);
+            return hip_fail(e, "hipEventCreateWithFlags");
+        }
         r->bands.push_back(b);
     }
     r->width = w;
     r->height = h;
+    r->stop_req.store(false);
+    r->bands_queued.store(0);
+    r->feed_rc.store(0);
+    r->feed_err.clear();
+    try {
+        r->feeder = std::thread(feed_bands, r);
+    } catch (const std::exception &ex) {
+        release_bands(r);
+        return fail(PT_ERR_INVALID, std::string("cannot start the band feeder: ") + ex.what());
+    }
     r->started = true;
     return PT_OK;
 }
 
-int pt_render_step(pt_renderer *r, double *rgb, int blocking) {
-    if (!r || !rgb) return fail(PT_ERR_INVALID, "null argument");
+// Renderer::render_step: copy every band finished since the last call into
+// rgb (linear f64) and / or rgba (display encode); 1 once the frame is complete.
+int pt_render_step_rgba8(pt_renderer *r, double *rgb, uint8_t *rgba, int blocking) {
+    if (!r || (!rgb && !rgba)) return fail(PT_ERR_INVALID, "null argument");
     if (!r->started) return fail(PT_ERR_STATE, "render_step before start_rendering");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
+    if (blocking) join_feeder(r);  // every band queued (or the feeder failed)
+    if (r->feed_rc.load()) {
+        join_feeder(r);
+        const int rc = r->feed_rc.load();
+        const std::string msg = r->feed_err;
+        (void)pt_render_stop(r);
+        return fail(rc, "queueing the frame: " + msg);
+    }
+    const uint32_t queued = r->bands_queued.load();
     bool done = true;
-    for (auto &b : r->bands) {
+    for (uint32_t k = 0; k < r->bands.size(); k++) {
+        auto &b = r->bands[k];
         if (b.copied) continue;
+        if (k >= queued) {  // not queued yet (non-blocking only)
+            done = false;
+            continue;
+        }
         if (blocking) {
             HIP_TRY(hipEventSynchronize(b.ev));
         } else {
@@ -338,12 +609,13 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking) {
             }
             if (q != hipSuccess) return hip_fail(q, "hipEventQuery");
         }
-        size_t off = (size_t)b.row0 * r->width * 3;
-        size_t n = (size_t)(b.row1 - b.row0) * r->width * 3;
-        HIP_TRY(hipMemcpy(rgb + off, r->d_frame + off, n * sizeof(double), hipMemcpyDeviceToHost));
+        const size_t p0 = (size_t)b.row0 * r->width, np = (size_t)(b.row1 - b.row0) * r->width;
+        if (rgb) HIP_TRY(hipMemcpy(rgb + p0 * 3, r->d_frame + p0 * 3, np * 3 * sizeof(double), hipMemcpyDeviceToHost));
+        if (rgba) HIP_TRY(hipMemcpy(rgba + p0 * 4, r->d_rgba + p0 * 4, np * 4, hipMemcpyDeviceToHost));
         b.copied = true;
     }
     if (done) {
+        join_feeder(r);
         release_bands(r);
         r->started = false;
         return 1;
@@ -351,13 +623,21 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking) {
     return 0;
 }
 
+int pt_render_step(pt_renderer *r, double *rgb, int blocking) {
+    if (!r || !rgb) return fail(PT_ERR_INVALID, "null argument");
+    return pt_render_step_rgba8(r, rgb, nullptr, blocking);
+}
+
+// Renderer::stop_rendering: the feeder queues no further band; the (at most
+// two) bands already queued drain; the frame is forgotten.
 int pt_render_stop(pt_renderer *r) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(r->device));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    r->stop_req.store(true);
+    join_feeder(r);
+    int rc = sync_all(r);
     release_bands(r);
     r->started = false;
-    return PT_OK;
+    return rc;
 }
 
 uint32_t pt_shard_tiles(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
@@ -371,23 +651,56 @@ int pt_render_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t 
     if (!r || !cam || !d_out) return fail(PT_ERR_INVALID, "null argument");
     if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
     if (world == 0 || rank >= world) return fail(PT_ERR_INVALID, "rank must be < world");
-    HIP_TRY(hipSetDevice(r->device));
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
+    GpuShare &g = r->gpus[0];
+    HIP_TRY(hipSetDevice(g.device));
     FrameParams P = frame_params(r, *cam, w, h, spp, seed);
     P.rank = rank;
     P.world = world;
     P.compact = world > 1 ? 1 : 0;
     P.tile_begin = 0;
     P.tile_count = pt_shard_tiles(w, h, rank, world);
-    // any HIP stream, 0 being the null stream as everywhere in HIP (pt_unshard_device
-    // takes the same handle, so a caller's render -> gather -> unshard stays ordered)
-    hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(launch_render(r->ds, P, d_out, st, &r->ws));
+    // any HIP stream of the renderer's (first) device, 0 being the null stream
+    // as everywhere in HIP (pt_unshard_device takes the same handle, so a
+    // caller's render -> gather -> unshard stays ordered)
+    HIP_TRY(launch_render(g.ds, P, d_out, (hipStream_t)stream, &g.ws));
     return PT_OK;
 }
 
-int pt_unshard_device(const double *g, uint32_t w, uint32_t h, uint32_t world, double *frame, void *stream) {
+int pt_render_frame_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
+                           double *d_frame, void *stream) {
+    if (!r || !cam || !d_frame) return fail(PT_ERR_INVALID, "null argument");
+    if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
+    GpuShare &g0 = r->gpus[0];
+    HIP_TRY(hipSetDevice(g0.device));
+    hipStream_t st = (hipStream_t)stream;
+    // the frame runs on the renderer's streams, after everything queued on st;
+    // st resumes when the frame is in d_frame
+    HIP_TRY(hipEventRecord(g0.shard_ev, st));
+    HIP_TRY(hipStreamWaitEvent(g0.stream, g0.shard_ev, 0));
+    const FrameParams P = frame_params(r, *cam, w, h, spp, seed);
+    if (int rc = frame_prologue(r, w, h)) return rc;
+    if (int rc = enqueue_band(r, P, d_frame, nullptr, 0, tiles_y_of(h), nullptr)) return rc;
+    HIP_TRY(hipSetDevice(g0.device));
+    HIP_TRY(hipEventRecord(g0.shard_ev, g0.stream));
+    HIP_TRY(hipStreamWaitEvent(st, g0.shard_ev, 0));
+    return PT_OK;
+}
+
+int pt_unshard_device(int device, const double *g, uint32_t w, uint32_t h, uint32_t world, double *frame,
+                      void *stream) {
     if (!g || !frame || world == 0) return fail(PT_ERR_INVALID, "bad argument");
+    if (device >= 0) HIP_TRY(hipSetDevice(device));
     HIP_TRY(launch_unshard(g, w, h, world, frame, (hipStream_t)stream));
+    return PT_OK;
+}
+
+int pt_encode_rgba8_device(int device, const double *d_rgb, size_t npix, uint8_t *d_rgba, void *stream) {
+    if (npix && (!d_rgb || !d_rgba)) return fail(PT_ERR_INVALID, "null argument");
+    if (((uintptr_t)d_rgba & 3u) != 0) return fail(PT_ERR_INVALID, "rgba must be 4-byte aligned");
+    if (device >= 0) HIP_TRY(hipSetDevice(device));
+    HIP_TRY(launch_encode_rgba8(d_rgb, 0, npix, d_rgba, (hipStream_t)stream));
     return PT_OK;
 }
 
@@ -395,14 +708,14 @@ int pt_unshard_device(const double *g, uint32_t w, uint32_t h, uint32_t world, d
 
 int pt_closest_hit(pt_renderer *r, const double *rays, size_t n, double min_t, double max_t, pt_hit *out) {
     if (!r || (n && (!rays || !out))) return fail(PT_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     DevBuf<double> dr;
     DevBuf<pt_hit> dh;
     HIP_TRY(dr.alloc(n * 6));
     HIP_TRY(dh.alloc(n));
     HIP_TRY(hipMemcpy(dr.p, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice));
-    HIP_TRY(launch_closest_hit(r->ds, dr.p, n, min_t, max_t, dh.p, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(launch_closest_hit(r->gpus[0].ds, dr.p, n, min_t, max_t, dh.p, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
     HIP_TRY(hipMemcpy(out, dh.p, n * sizeof(pt_hit), hipMemcpyDeviceToHost));
     return PT_OK;
 }
@@ -410,7 +723,7 @@ int pt_closest_hit(pt_renderer *r, const double *rays, size_t n, double min_t, d
 int pt_ray_color(pt_renderer *r, const double *rays, uint64_t *states, size_t n, uint32_t depth, double *out) {
     if (!r || (n && (!rays || !states || !out))) return fail(PT_ERR_INVALID, "null argument");
     if (depth > 64) return fail(PT_ERR_UNSUPPORTED, "depth > 64 is not supported on the GPU path");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     DevBuf<double> dr, dout;
     DevBuf<uint64_t> ds;
     HIP_TRY(dr.alloc(n * 6));
@@ -418,8 +731,8 @@ int pt_ray_color(pt_renderer *r, const double *rays, uint64_t *states, size_t n,
     HIP_TRY(dout.alloc(n * 3));
     HIP_TRY(hipMemcpy(dr.p, rays, n * 6 * sizeof(double), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(ds.p, states, n * sizeof(uint64_t), hipMemcpyHostToDevice));
-    HIP_TRY(launch_ray_color(r->ds, dr.p, ds.p, n, depth, r->s11, dout.p, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(launch_ray_color(r->gpus[0].ds, dr.p, ds.p, n, depth, r->s11, dout.p, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
     HIP_TRY(hipMemcpy(out, dout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(states, ds.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PT_OK;
@@ -431,15 +744,15 @@ int pt_trace_pixel_samples(pt_renderer *r, const pt_camera *cam, uint32_t w, uin
     if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
     for (size_t i = 0; i < n; i++)
         if (pixels[i] >= (uint64_t)w * h) return fail(PT_ERR_INVALID, "pixel index out of range");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     FrameParams P = frame_params(r, *cam, w, h, spp, seed);
     DevBuf<uint32_t> dp;
     DevBuf<double> dout;
     HIP_TRY(dp.alloc(n));
     HIP_TRY(dout.alloc(n * 3));
     HIP_TRY(hipMemcpy(dp.p, pixels, n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(launch_trace_pixels(r->ds, P, dp.p, n, dout.p, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(launch_trace_pixels(r->gpus[0].ds, P, dp.p, n, dout.p, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
     HIP_TRY(hipMemcpy(out, dout.p, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
     return PT_OK;
 }
@@ -451,16 +764,16 @@ int pt_count_work(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, 
     if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
     for (size_t i = 0; i < n; i++)
         if (pixels[i] >= (uint64_t)w * h) return fail(PT_ERR_INVALID, "pixel index out of range");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     FrameParams P = frame_params(r, *cam, w, h, spp, seed);
     DevBuf<uint32_t> dp;
     DevBuf<unsigned long long> dc;
     HIP_TRY(dp.alloc(n));
     HIP_TRY(dc.alloc(C_COUNT));
     HIP_TRY(hipMemcpy(dp.p, pixels, n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemsetAsync(dc.p, 0, C_COUNT * sizeof(unsigned long long), r->stream));
-    HIP_TRY(launch_count_work(r->ds, P, dp.p, n, dc.p, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(hipMemsetAsync(dc.p, 0, C_COUNT * sizeof(unsigned long long), r->stream()));
+    HIP_TRY(launch_count_work(r->gpus[0].ds, P, dp.p, n, dc.p, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
     HIP_TRY(hipMemcpy(counters, dc.p, C_COUNT * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }
@@ -468,7 +781,7 @@ int pt_count_work(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, 
 int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, int32_t *status, uint32_t *iters) {
     if (!r || (n && (!jobs || !t_out || !status || !iters))) return fail(PT_ERR_INVALID, "null argument");
     if (n == 0) return PT_OK;
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     DevBuf<double> dj, dt;
     DevBuf<int32_t> ds;
     DevBuf<uint32_t> di;
@@ -476,43 +789,58 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
     HIP_TRY(dt.alloc(n));
     HIP_TRY(ds.alloc(n));
     HIP_TRY(di.alloc(n));
-    HIP_TRY(hipMemcpyAsync(dj.p, jobs, n * 8 * sizeof(double), hipMemcpyHostToDevice, r->stream));
-    HIP_TRY(launch_march_probe(dj.p, n, dt.p, ds.p, di.p, r->stream));
-    HIP_TRY(hipMemcpyAsync(t_out, dt.p, n * sizeof(double), hipMemcpyDeviceToHost, r->stream));
-    HIP_TRY(hipMemcpyAsync(status, ds.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream));
-    HIP_TRY(hipMemcpyAsync(iters, di.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(hipMemcpyAsync(dj.p, jobs, n * 8 * sizeof(double), hipMemcpyHostToDevice, r->stream()));
+    HIP_TRY(launch_march_probe(dj.p, n, dt.p, ds.p, di.p, r->stream()));
+    HIP_TRY(hipMemcpyAsync(t_out, dt.p, n * sizeof(double), hipMemcpyDeviceToHost, r->stream()));
+    HIP_TRY(hipMemcpyAsync(status, ds.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, r->stream()));
+    HIP_TRY(hipMemcpyAsync(iters, di.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
+    return PT_OK;
+}
+
+int pt_march_guard_drops(pt_renderer *r, uint64_t *count) {
+    if (!r || !count) return fail(PT_ERR_INVALID, "null argument");
+    uint64_t total = 0;
+    for (auto &g : r->gpus) {
+        HIP_TRY(hipSetDevice(g.device));
+        HIP_TRY(hipDeviceSynchronize());  // frames on any stream of the device
+        unsigned long long n = 0;
+        HIP_TRY(hipMemcpy(&n, g.ds.guard, sizeof n, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(g.ds.guard, 0, sizeof n));
+        total += n;
+    }
+    *count = total;
     return PT_OK;
 }
 
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     double m[K_KINDS];
     uint32_t l[K_KINDS];
-    HIP_TRY(timer_collect(r->ws.timer, m, l));
+    HIP_TRY(timer_collect(r->gpus[0].ws.timer, m, l));
     for (size_t k = 0; k < nkinds && k < (size_t)K_KINDS; k++) {
         if (ms) ms[k] = m[k];
         if (launches) launches[k] = l[k];
     }
-    if (enable && !r->ws.timer) r->ws.timer = timer_new();
-    if (!enable && r->ws.timer) {
-        timer_free(r->ws.timer);
-        r->ws.timer = nullptr;
+    if (enable && !r->gpus[0].ws.timer) r->gpus[0].ws.timer = timer_new();
+    if (!enable && r->gpus[0].ws.timer) {
+        timer_free(r->gpus[0].ws.timer);
+        r->gpus[0].ws.timer = nullptr;
     }
     return PT_OK;
 }
 
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(r->device));
-    HIP_TRY(hipStreamSynchronize(r->stream));
-    if (out && n && r->ws.diag) HIP_TRY(hipMemcpy(out, r->ws.diag, (n < 40 ? n : 40) * 8, hipMemcpyDeviceToHost));
-    if (enable && !r->ws.diag) HIP_TRY(hipMalloc(&r->ws.diag, 40 * 8));
-    if (r->ws.diag) HIP_TRY(hipMemset(r->ws.diag, 0, 40 * 8));
-    if (!enable && r->ws.diag) {
-        HIP_TRY(hipFree(r->ws.diag));
-        r->ws.diag = nullptr;
+    HIP_TRY(hipSetDevice(r->device()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
+    if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 40 ? n : 40) * 8, hipMemcpyDeviceToHost));
+    if (enable && !r->gpus[0].ws.diag) HIP_TRY(hipMalloc(&r->gpus[0].ws.diag, 40 * 8));
+    if (r->gpus[0].ws.diag) HIP_TRY(hipMemset(r->gpus[0].ws.diag, 0, 40 * 8));
+    if (!enable && r->gpus[0].ws.diag) {
+        HIP_TRY(hipFree(r->gpus[0].ws.diag));
+        r->gpus[0].ws.diag = nullptr;
     }
     return PT_OK;
 }
@@ -521,16 +849,16 @@ int pt_profile_phases(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t
                       uint64_t *out) {
     if (!r || !cam || !out) return fail(PT_ERR_INVALID, "null argument");
     if (r->depth > 8) return fail(PT_ERR_UNSUPPORTED, "phase profiling supports depth <= 8");
-    HIP_TRY(hipSetDevice(r->device));
+    HIP_TRY(hipSetDevice(r->device()));
     FrameParams P = frame_params(r, *cam, w, h, spp, seed);
     P.tile_count = pt_shard_tiles(w, h, 0, 1);
     DevBuf<double> frame;
     DevBuf<unsigned long long> acc;
     HIP_TRY(frame.alloc((size_t)w * h * 3));
     HIP_TRY(acc.alloc(10));
-    HIP_TRY(hipMemsetAsync(acc.p, 0, 10 * sizeof(unsigned long long), r->stream));
-    HIP_TRY(launch_render_timed(r->ds, P, frame.p, acc.p, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));
+    HIP_TRY(hipMemsetAsync(acc.p, 0, 10 * sizeof(unsigned long long), r->stream()));
+    HIP_TRY(launch_render_timed(r->gpus[0].ds, P, frame.p, acc.p, r->stream()));
+    HIP_TRY(hipStreamSynchronize(r->stream()));
     HIP_TRY(hipMemcpy(out, acc.p, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PT_OK;
 }

@@ -161,12 +161,22 @@ struct Ray {
 #ifndef PT_LIN_BOX
 #define PT_LIN_BOX 1  // padded-box pre-test for cubes and spheres on the wave-uniform list
 #endif
+// Counts a march dropped by the march guard (pt_march_guard_drops).
+PT_HD void note_guard(unsigned long long *guard) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (guard) atomicAdd(guard, 1ull);
+#else
+    if (guard) ++*guard;
+#endif
+}
+
 // MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
 // every one on the march list), so the march branch is not compiled in.
 // EXT: the extended build (scenes with a Torus or non-solid textures) that
 // also carries the Torus' quartic; other builds never see a Torus.
 template <bool STATS, int FK = march::F_ANY, bool MARCHED = true, bool EXT = false>
-PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct) {
+PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct,
+                      unsigned long long *guard = nullptr) {
     if (STATS) ct->c[s.type == TORUS ? C_TEST_TORUS : C_TEST_SPHERE + s.type]++;
     if (PT_LAZY_RECT && s.type == RECTANGLE) {
         // Rectangle: t needs only the object-space z row; x and y are
@@ -197,13 +207,15 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         return torus::torus_t(s.p[0], s.p[1], o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t, t);
     default: {
         if (!MARCHED) return false;
-        march::MarchStats ms{0, 0, 0};
+        march::MarchStats ms{0, 0, 0, 0};
         bool h = march::func_march<STATS, FK>(shape_params(s), s.p[0], s.depth, o.x, o.y, o.z, d.x, d.y, d.z, min_t, max_t,
                                           t, &ms);
+        if (ms.guard) note_guard(guard);
         if (STATS) {
             ct->c[C_MARCH_STEPS] += ms.steps;
             ct->c[C_MARCH_BLOCKS] += ms.blocks;
             ct->c[C_MARCH_TRIES] += ms.tries;
+            ct->c[C_MARCH_GUARD] += ms.guard;
         }
         return h;
     }
@@ -255,12 +267,12 @@ PT_HD DBox uniform_box(const DBox *p) {
 // logical tile k sits at column (k % tiles_x + row) % tiles_x of its row, so a
 // rank's columns shift by one per row (a diagonal deal) instead of repeating
 // in every row when tiles_x is a multiple of world.  world == 1: identity.
-PT_HD inline uint32_t tile_position(uint32_t k, uint32_t tiles_x, uint32_t world) {
+PT_HD uint32_t tile_position(uint32_t k, uint32_t tiles_x, uint32_t world) {
     if (world <= 1) return k;
     const uint32_t ty = k / tiles_x;
     return ty * tiles_x + (k % tiles_x + ty) % tiles_x;
 }
-PT_HD inline uint32_t tile_logical(uint32_t p, uint32_t tiles_x, uint32_t world) {
+PT_HD uint32_t tile_logical(uint32_t p, uint32_t tiles_x, uint32_t world) {
     if (world <= 1) return p;
     const uint32_t ty = p / tiles_x;
     return ty * tiles_x + (p % tiles_x + tiles_x - ty % tiles_x) % tiles_x;
@@ -280,7 +292,11 @@ struct Scene {
     const uint8_t *__restrict__ pixels;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
     int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
+    // marches dropped by the march guard (pt_march.hpp MARCH_GUARD), counted
+    // on the device (pt_march_guard_drops); null: not counted
+    unsigned long long *guard;
 };
+
 
 // Padded-box slab test against [min_t, max_t] (conservative: boxes are padded
 // far beyond the rounding of this test).
@@ -363,7 +379,7 @@ PT_HD int closest(const Scene &sc, const Ray &r, double min_t, double max_t, dou
         if (STATS) ct->c[C_MARCH_SLABS]++;
         if (!slab(b.lo, b.hi, r, inv, min_t, best)) continue;
         double t;
-        if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
+        if (shape_test<STATS>(sc.shapes[i], r, min_t, best, &t, ct, sc.guard) && (t < best || i > who)) {
             best = t;
             who = i;
         }
@@ -781,7 +797,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
     double best = 0.0;
     V3 inv = v3(0.0, 0.0, 0.0);
     march::MarchState ms;
-    march::MarchStats mst{0, 0, 0};
+    march::MarchStats mst{0, 0, 0, 0};
     uint64_t ts = 0;
     for (;;) {
         if (TIMING) {
@@ -807,6 +823,10 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
             for (int it = 0; it < MARCH_ITERS; it++) {
                 int st = march::march_iter<STATS, true, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
+                    if (st == march::M_GUARD) {
+                        note_guard(sc.guard);
+                        if (STATS) ct->c[C_MARCH_GUARD]++;
+                    }
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                     if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
                         best = ms.t;

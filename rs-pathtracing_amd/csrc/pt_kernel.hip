@@ -12,6 +12,7 @@
 #include "pt_kernel.hpp"
 
 #include <cstdlib>
+#include <cstring>
 
 #ifndef PT_DEFAULT_WAVES
 #define PT_DEFAULT_WAVES 4  // C5 (100k spheres, compact BVH): 2 waves 845-849, 3: 1044, 4: 1109 M samples/s
@@ -44,10 +45,13 @@ __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameP
     dst[2] = c.z;
 }
 
-__global__ void unshard(const double *__restrict__ g, uint32_t width, uint32_t height, uint32_t world,
-                        uint32_t tiles_x, uint32_t per_rank, double *__restrict__ frame) {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)width * height) return;
+// Rows [y0, y1) of the frame from the gathered rank shards (rank-major, each
+// padded to per_rank tiles): 48 B moved per pixel, HBM-bound.
+__global__ __launch_bounds__(256) void unshard(const double *__restrict__ g, uint32_t width, uint32_t y0, uint32_t y1,
+                                               uint32_t world, uint32_t tiles_x, uint32_t per_rank,
+                                               double *__restrict__ frame) {
+    const size_t i = (size_t)y0 * width + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)y1 * width) return;
     uint32_t x = (uint32_t)(i % width), y = (uint32_t)(i / width);
     uint32_t k = dev::tile_logical((y / TILE) * tiles_x + x / TILE, tiles_x, world);
     uint32_t rank = k % world, ti = k / world;
@@ -55,6 +59,27 @@ __global__ void unshard(const double *__restrict__ g, uint32_t width, uint32_t h
     frame[i * 3 + 0] = s[0];
     frame[i * 3 + 1] = s[1];
     frame[i * 3 + 2] = s[2];
+}
+
+// Display encode of the GUI loop (src/bin/main.rs:281-289, main_raylib.rs:239-247):
+// per channel sqrt -> f64::clamp(0, 0.999) -> *256 -> `as u8`, alpha 255.
+// f64::clamp passes NaN through and the saturating `as u8` cast maps NaN to 0
+// (and anything >= 256 to 255, which the clamp already prevents).  One pixel
+// per lane: 24 B read, 4 B written, HBM-bound.
+__device__ __forceinline__ uint32_t encode_channel(double c) {
+    double v = sqrt(c);
+    v = v < 0.0 ? 0.0 : v;  // Rust's clamp: if self < min { min }; if self > max { max }
+    v = v > 0.999 ? 0.999 : v;
+    const double s = v * 256.0;
+    return s != s ? 0u : (uint32_t)s;  // NaN -> 0; 0 <= s < 256 otherwise
+}
+__global__ __launch_bounds__(256) void encode_rgba8(const double *__restrict__ rgb, size_t p0, size_t p1,
+                                                    uint32_t *__restrict__ rgba) {
+    const size_t i = p0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p1) return;
+    const uint32_t r = encode_channel(rgb[i * 3 + 0]), g = encode_channel(rgb[i * 3 + 1]),
+                   b = encode_channel(rgb[i * 3 + 2]);
+    rgba[i] = r | (g << 8) | (b << 16) | (255u << 24);  // bytes R, G, B, A in memory order
 }
 
 __global__ __launch_bounds__(256) void closest_hit_probe(dev::Scene sc, const double *__restrict__ rays, size_t n, double min_t,
@@ -149,11 +174,11 @@ __global__ __launch_bounds__(256) void march_probe(const double *__restrict__ jo
     march::FParams F{};
     F.func = march::F_HEART;
     if (march::march_begin(F, j[0], (int)j[1], j[2], j[3], j[4], j[5], j[6], j[7], &m)) {
-        march::MarchStats ms{0, 0, 0};
+        march::MarchStats ms{0, 0, 0, 0};
         while ((st = march::march_iter<false>(m, &ms)) == march::M_RUNNING) k++;
     }
     t_out[i] = m.t;
-    status[i] = st == march::M_DONE ? 1 : 0;
+    status[i] = st == march::M_DONE ? 1 : (st == march::M_GUARD ? 2 : 0);
     iters[i] = k;
 }
 
@@ -216,11 +241,8 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.nnodes = s.nnodes;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
-    static int diag = [] {
-        const char *e = getenv("PT_DIAG");
-        return e ? atoi(e) : 0;
-    }();
-    d.diag = diag;
+    d.diag = s.diag;
+    d.guard = s.guard;
     return d;
 }
 
@@ -242,16 +264,82 @@ static dev::Scene dscene(const DeviceScene &s) {
         }                                  \
     } while (0)
 
-// Occupancy variant of render_tiles (PT_WAVES=2|3|4|5 in the environment, read
-// once; default below).  Depths > 8 use the 2-wave build: their attenuation
-// stacks are wider.
-static int render_waves() {
-    static int w = [] {
-        const char *e = getenv("PT_WAVES");
-        int v = e ? atoi(e) : PT_DEFAULT_WAVES;
-        return (v >= 2 && v <= 5) ? v : PT_DEFAULT_WAVES;
-    }();
-    return w;
+// ------------------------------------------------------------- tuning
+const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
+                                    "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
+                                    "wf_march_blocks_per_cu", nullptr};
+
+static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
+    struct F {
+        const char *n;
+        int Tuning::*i;
+        int64_t lo, hi;
+    };
+    static const F fs[] = {
+        {"engine", &Tuning::engine, 0, 2},
+        {"mega_waves", &Tuning::mega_waves, 2, 5},
+        {"diag", &Tuning::diag, 0, 1},
+        {"wf_slots", &Tuning::wf_slots, 1, WaveWorkspace::MAX_SLOTS},
+        {"wf_min_chunks", &Tuning::wf_min_chunks, 1, 4096},
+        {"wf_bounce_waves", &Tuning::wf_bounce_waves, 2, 8},
+        {"wf_fused", &Tuning::wf_fused, 0, 1},
+        {"wf_march_slice", &Tuning::wf_march_slice, 0, 1 << 20},
+        {"wf_trace_slice", &Tuning::wf_trace_slice, 1, 1 << 20},
+        {"wf_march_blocks_per_cu", &Tuning::wf_march_blocks_per_cu, 0, 64},
+    };
+    *iv = nullptr;
+    if (!name) return nullptr;
+    if (!strcmp(name, "wf_paths")) {
+        *lo = 256;
+        *hi = (int64_t)1 << 28;
+        return &t->wf_paths;
+    }
+    for (const F &f : fs)
+        if (!strcmp(name, f.n)) {
+            *lo = f.lo;
+            *hi = f.hi;
+            *iv = &(t->*(f.i));
+            return nullptr;
+        }
+    return nullptr;
+}
+
+int tuning_set(Tuning *t, const char *name, int64_t v) {
+    int64_t lo = 0, hi = 0;
+    int *iv = nullptr;
+    int64_t *lv = tuning_field(t, name, &lo, &hi, &iv);
+    if (!lv && !iv) return PT_ERR_INVALID;
+    if (v < lo || v > hi) return PT_ERR_INVALID;
+    if (!strcmp(name, "wf_bounce_waves") && !(v == 2 || v == 3 || v == 4 || v == 5 || v == 6 || v == 8))
+        return PT_ERR_INVALID;
+    if (lv) *lv = v;
+    else *iv = (int)v;
+    return PT_OK;
+}
+
+int tuning_get(const Tuning &t0, const char *name, int64_t *v) {
+    Tuning t = t0;
+    int64_t lo = 0, hi = 0;
+    int *iv = nullptr;
+    int64_t *lv = tuning_field(&t, name, &lo, &hi, &iv);
+    if (!lv && !iv) return PT_ERR_INVALID;
+    *v = lv ? *lv : (int64_t)*iv;
+    return PT_OK;
+}
+
+Tuning tuning_from_env() {
+    Tuning t;
+    static const struct {
+        const char *env, *name;
+    } map[] = {{"PT_WAVES", "mega_waves"}, {"PT_DIAG", "diag"}, {"PT_WF_SLOTS", "wf_slots"},
+               {"PT_WF_PATHS", "wf_paths"}, {"PT_WF_MIN_CHUNKS", "wf_min_chunks"},
+               {"PT_WF_BOUNCE_WAVES", "wf_bounce_waves"}, {"PT_WF_FUSED", "wf_fused"},
+               {"PT_WF_MARCH_SLICE", "wf_march_slice"}, {"PT_WF_TRACE_SLICE", "wf_trace_slice"},
+               {"PT_WF_MARCH_BLOCKS_PER_CU", "wf_march_blocks_per_cu"}};
+    for (const auto &m : map)
+        if (const char *e = getenv(m.env)) (void)tuning_set(&t, m.name, atoll(e));  // out of range: default kept
+    if (const char *e = getenv("PT_ENGINE")) t.engine = e[0] == 'm' ? 1 : (e[0] == 'w' ? 2 : 0);
+    return t;
 }
 
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
@@ -259,10 +347,10 @@ hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double
 
 static bool use_wavefront(const DeviceScene &s, WaveWorkspace *ws) {
     if (s.ext) return true;  // textures / Torus: the extended builds live in the wavefront engine
-    const char *e = getenv("PT_ENGINE");
-    if (e && e[0] == 'm') return false;
-    if (e && e[0] == 'w') return ws != nullptr;
-    return ws != nullptr && s.nmarch > 0 && (dscene(s).diag & 1) == 0;
+    const int engine = ws ? ws->tune.engine : 1;
+    if (engine == 1) return false;
+    if (engine == 2) return ws != nullptr;
+    return ws != nullptr && s.nmarch > 0 && (s.diag & 1) == 0;
 }
 
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
@@ -274,7 +362,9 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
     if (e0 != hipSuccess) return e0;
     if (P.depth <= 8 && s.fkind == march::F_HEART) {
         // Heart-only (or no marched shape): the single-function build
-        switch (render_waves()) {
+        // megakernel register budget (Tuning::mega_waves); depths > 8 use the
+        // 2-wave build: their attenuation stacks are wider
+        switch (ws ? ws->tune.mega_waves : PT_DEFAULT_WAVES) {
         case 2: render_tiles<4, 2, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         case 3: render_tiles<4, 3, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         case 5: render_tiles<4, 5, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
@@ -291,13 +381,20 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
 }
 
 hipError_t launch_unshard(const double *g, uint32_t width, uint32_t height, uint32_t world, double *frame,
-                          hipStream_t st) {
+                          hipStream_t st, uint32_t y0, uint32_t y1) {
     uint32_t tiles_x = (width + TILE - 1) / TILE, tiles_y = (height + TILE - 1) / TILE;
     uint32_t total = tiles_x * tiles_y;
     uint32_t per_rank = (total + world - 1) / world;
-    size_t npix = (size_t)width * height;
-    unsigned blocks = (unsigned)((npix + 255) / 256);
-    if (blocks) unshard<<<blocks, 256, 0, st>>>(g, width, height, world, tiles_x, per_rank, frame);
+    if (y1 > height) y1 = height;
+    if (y0 >= y1) return hipSuccess;
+    size_t npix = (size_t)width * (y1 - y0);
+    unshard<<<(unsigned)((npix + 255) / 256), 256, 0, st>>>(g, width, y0, y1, world, tiles_x, per_rank, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_encode_rgba8(const double *rgb, size_t p0, size_t p1, uint8_t *rgba, hipStream_t st) {
+    if (p1 <= p0) return hipSuccess;
+    encode_rgba8<<<(unsigned)((p1 - p0 + 255) / 256), 256, 0, st>>>(rgb, p0, p1, (uint32_t *)rgba);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ struct DeviceScene {
     int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
     int ext = 0;    // non-solid textures or a Torus: the extended (EXT) kernel builds
     int fkind = 0;  // 0: every marched shape is a Heart (or none) -> Heart-only kernel builds; -1: any
+    int diag = 0;  // Tuning::diag (timing ablation), copied here for the probes
+    unsigned long long *guard = nullptr;  // device counter of marches dropped by the march guard
 };
 
 // Device workspace of the wavefront engine (pt_wave.hip), grown on demand and
@@ -34,7 +36,31 @@ hipError_t timer_begin(KernelTimer *t, hipStream_t st, int kind);  // no-op when
 hipError_t timer_end(KernelTimer *t, hipStream_t st);
 hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches);  // sums since last collect
 
+// Tuning knobs of the render engines (pt_renderer_set_option).  The defaults
+// are the measured optimum on MI355X.  A renderer takes its
+// initial values from the PT_* environment variables named below, once, when
+// it is created; bench.py reports every knob that differs from its default.
+struct Tuning {
+    int engine = 0;                  // PT_ENGINE: 0 auto (wavefront iff the scene marches), 1 megakernel, 2 wavefront
+    int mega_waves = 4;              // PT_WAVES: megakernel register budget, waves per SIMD (2..5)
+    int diag = 0;                    // PT_DIAG bit 0: skip ray-marched shapes (a timing ablation, not the reference)
+    int wf_slots = 2;                // PT_WF_SLOTS: sample chunks in flight, one stream each (1..4)
+    int64_t wf_paths = 1 << 24;      // PT_WF_PATHS: path slots per chunk (256 .. 2^28)
+    int wf_min_chunks = 1;           // PT_WF_MIN_CHUNKS: at least this many sample chunks per frame (1..4096)
+    int wf_bounce_waves = 3;         // PT_WF_BOUNCE_WAVES: wf_bounce register budget (2, 3, 4, 5, 6, 8)
+    int wf_fused = 0;                // PT_WF_FUSED: fused bounces (wf_trace) instead of one launch per bounce
+    int wf_march_slice = 256;        // PT_WF_MARCH_SLICE: march-queue run dealt to a block (0 = contiguous share)
+    int wf_trace_slice = 256;        // PT_WF_TRACE_SLICE: live-list run dealt to a wf_trace block
+    int wf_march_blocks_per_cu = 0;  // PT_WF_MARCH_BLOCKS_PER_CU: persistent march grid (0 = occupancy maximum)
+};
+Tuning tuning_from_env();
+// 0 on success, PT_ERR_INVALID for an unknown name or a value out of range
+int tuning_set(Tuning *t, const char *name, int64_t value);
+int tuning_get(const Tuning &t, const char *name, int64_t *value);
+extern const char *const TUNING_NAMES[];  // null-terminated
+
 struct WaveWorkspace {
+    Tuning tune;  // this renderer's knobs (both engines read them from here)
     void *base = nullptr;
     size_t bytes = 0;
     unsigned long long *diag = nullptr;  // march-kernel phase diagnostics (pt_wave_diag), when enabled
@@ -44,6 +70,10 @@ struct WaveWorkspace {
     static constexpr int MAX_SLOTS = 4;
     hipStream_t side[MAX_SLOTS - 1] = {};
     hipEvent_t fork = nullptr, join[MAX_SLOTS - 1] = {}, reduced = nullptr;
+    // recorded on the launch stream after a frame's last use of the workspace;
+    // the next frame (on any stream) waits for it
+    hipEvent_t done = nullptr;
+    bool used = false;
     int device = -1;
 };
 void wave_workspace_free(WaveWorkspace *ws);
@@ -53,8 +83,11 @@ void wave_workspace_free(WaveWorkspace *ws);
 // PT_ENGINE=wave in the environment forces one.
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
                          WaveWorkspace *ws);
+// rows [y0, y1) of the frame from gathered shards (pt_unshard_device)
 hipError_t launch_unshard(const double *gathered, uint32_t width, uint32_t height, uint32_t world, double *frame,
-                          hipStream_t st);
+                          hipStream_t st, uint32_t y0 = 0, uint32_t y1 = ~0u);
+// display encode of pixels [p0, p1) (pt_encode_rgba8_device); rgba is 4-byte aligned
+hipError_t launch_encode_rgba8(const double *rgb, size_t p0, size_t p1, uint8_t *rgba, hipStream_t st);
 hipError_t launch_closest_hit(const DeviceScene &s, const double *rays, size_t n, double min_t, double max_t,
                               pt_hit *out, hipStream_t st);
 hipError_t launch_ray_color(const DeviceScene &s, const double *rays, uint64_t *states, size_t n, uint32_t depth,

@@ -535,6 +535,7 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
 #endif
 struct MarchStats {
     uint32_t steps, blocks, tries;
+    uint32_t guard;  // marches dropped by the MARCH_GUARD (always counted, not only in STATS builds)
 };
 
 // Resumable form of RayMarchingShape::ray_intersect (ray_marching.rs:20-74) so
@@ -550,7 +551,9 @@ struct MarchState {
     int lit;         // literal steps to take before the next proof attempt (the crossing is near)
     double na[4];    // steps still to apply to t, px, py, pz during an advance
 };
-enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2 };
+// M_GUARD: the march was dropped by MARCH_GUARD (callers take it as a miss
+// and count it: pt_march_guard_drops).
+enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2, M_GUARD = 3 };
 constexpr uint32_t MARCH_GUARD = 1u << 24;
 
 // Bound test and start of the march; false if the ray misses the bound.
@@ -608,8 +611,9 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
     if (m.pass >= m.passes) return M_DONE;
     // Every iteration takes >= 1 reference step; a march still running after
     // 2^24 of them is one the reference itself would not finish (a step below
-    // t's rounding, say).  Dropping it keeps every GPU wave finite.
-    if (++m.iters > MARCH_GUARD) return M_MISS;
+    // t's rounding, say: t + step == t forever).  Dropping it keeps every GPU
+    // wave finite; the caller counts the drop (M_GUARD) and takes it as a miss.
+    if (++m.iters > MARCH_GUARD) return M_GUARD;
     double s = m.s;
     double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
     if (m.adv) {
@@ -721,7 +725,8 @@ PT_HD bool func_march(const FParams &F, double step0, int passes, double ox, dou
     int status;
     while ((status = march_iter<STATS, true, FK>(m, st)) == M_RUNNING) {
     }
-    if (status == M_MISS) return false;
+    if (status == M_GUARD) st->guard++;
+    if (status != M_DONE) return false;
     if (m.t < min_t || m.t > max_t) return false;  // ray_marching.rs:55-57
     *t_out = m.t;
     return true;

@@ -96,7 +96,7 @@ struct FrameParams {
 enum Counter : int {
     C_SAMPLES, C_BOUNCES, C_TEST_SPHERE, C_TEST_RECT, C_TEST_CUBE, C_TEST_MARCH, C_NODE_SLABS, C_MARCH_SLABS,
     C_MARCH_STEPS, C_MARCH_TRIES, C_MARCH_BLOCKS, C_HITS, C_LAMBERT, C_METAL, C_DIELECTRIC, C_REJECT_TRIES,
-    C_UNWIND, C_TEST_TORUS, C_COUNT
+    C_UNWIND, C_TEST_TORUS, C_MARCH_GUARD, C_COUNT
 };
 struct Ctr {
     uint64_t c[C_COUNT];

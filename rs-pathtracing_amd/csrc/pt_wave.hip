@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     int km = 0, mshape = -1;
     V3 inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchState ms;
-    march::MarchStats mst{0, 0, 0};
+    march::MarchStats mst{0, 0, 0, 0};
     unsigned long long dtrips[16], dcyc[16], dlanes[4];
     if (DIAG) {
         for (int k = 0; k < 16; k++) dtrips[k] = dcyc[k] = 0;
@@ -582,6 +582,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             if (marching) {
                 const int st = march::march_iter<false, PT_WF_VOTE == 0, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
+                    if (st == march::M_GUARD) dev::note_guard(sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                     if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
                         (ms.t < cur.best || mshape > cur.who)) {
@@ -720,12 +721,6 @@ hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches) {
 }
 
 // ------------------------------------------------------------- host driver
-static uint32_t wf_cap_paths() {
-    const char *e = getenv("PT_WF_PATHS");
-    long v = e ? atol(e) : (1l << 24);
-    return (uint32_t)(v < 256 ? 256 : (v > (1l << 28) ? (1l << 28) : v));
-}
-
 void wave_workspace_free(WaveWorkspace *ws) {
     for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
         if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
@@ -735,7 +730,9 @@ void wave_workspace_free(WaveWorkspace *ws) {
     }
     if (ws->fork) (void)hipEventDestroy(ws->fork);
     if (ws->reduced) (void)hipEventDestroy(ws->reduced);
-    ws->fork = ws->reduced = nullptr;
+    if (ws->done) (void)hipEventDestroy(ws->done);
+    ws->fork = ws->reduced = ws->done = nullptr;
+    ws->used = false;
     timer_free(ws->timer);
     ws->timer = nullptr;
     if (ws->diag) (void)hipFree(ws->diag);
@@ -747,7 +744,12 @@ void wave_workspace_free(WaveWorkspace *ws) {
 
 static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
     if (bytes <= ws->bytes) return hipSuccess;
-    // grow the path storage only; an enabled timer or diag buffer stays
+    // grow the path storage only; an enabled timer or diag buffer stays.  The
+    // previous frame (possibly on another stream) must be done with it first.
+    if (ws->used) {
+        hipError_t e = hipEventSynchronize(ws->done);
+        if (e != hipSuccess) return e;
+    }
     if (ws->base) (void)hipFree(ws->base);
     ws->base = nullptr;
     ws->bytes = 0;
@@ -760,15 +762,9 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
     return hipSuccess;
 }
 
-static int bounce_waves() {
-    const char *e = getenv("PT_WF_BOUNCE_WAVES");
-    const int w = e ? atoi(e) : PT_WF_BOUNCE_WAVES;
-    return w >= 2 && w <= 8 ? w : PT_WF_BOUNCE_WAVES;
-}
-
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
-                          const WfView &v, int it, unsigned long long *diag, int fkind) {
+                          const WfView &v, int it, unsigned long long *diag, int fkind, int waves) {
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
         wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
@@ -785,7 +781,7 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
         wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
     }
-    switch (bounce_waves()) {
+    switch (waves) {  // Tuning::wf_bounce_waves
     case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
     case 5: wf_bounce<NW, FIRST, 5, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
@@ -807,30 +803,15 @@ static uint32_t resident_blocks(K kern) {
     return (uint32_t)(cus * occ);
 }
 
-// The fused bounce step (wf_trace) only with PT_WF_FUSED=1 in the environment
-// (read per render).  Measured on C2: 1119 M samples/s fused against 1176 with
-// one wf_bounce launch per bounce — the bounce is VALU-bound, not bound by the
-// path-state traffic fusion removes, and the per-bounce launches interleave
-// better with the other chunk's marches — so per-bounce launches are the
-// default.  The diag build always runs wf_bounce.
-static bool fused_bounces() {
-    const char *e = getenv("PT_WF_FUSED");
-    return e && e[0] == '1';
-}
-
-static uint32_t trace_slice() {
-    static const uint32_t s = [] {
-        const char *e = getenv("PT_WF_TRACE_SLICE");  // tuning knob: ids per run dealt to a block
-        const long v = e ? atol(e) : 256;
-        return (uint32_t)(v < 1 ? 1 : (v > (1l << 20) ? (1l << 20) : v));
-    }();
-    return s;
-}
-
+// The fused bounce step (wf_trace) only with Tuning::wf_fused.  Measured on C2:
+// 1119 M samples/s fused against 1176 with one wf_bounce launch per bounce —
+// the bounce is VALU-bound, not bound by the path-state traffic fusion
+// removes, and the per-bounce launches interleave better with the other
+// chunk's marches — so per-bounce launches are the default.  The diag build
+// always runs wf_bounce.
 template <bool FIRST>
 static void launch_trace(hipStream_t st, const dev::Scene &sc, const FrameParams &P, const WfView &v, int it,
-                         int fkind) {
-    const uint32_t slice = trace_slice();
+                         int fkind, uint32_t slice) {
     if (sc.ext) {
         static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY, true>);
         wf_trace<FIRST, 2, march::F_ANY, true><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
@@ -843,16 +824,10 @@ static void launch_trace(hipStream_t st, const dev::Scene &sc, const FrameParams
     }
 }
 
-// Chunks in flight: each has its own path state (slot) and runs on its own
-// stream, so one chunk's bounce/compaction kernels fill the tails of the
-// other's march kernels (and its memory-bound bounces overlap the other's
-// VALU-bound marches).  Only the reduces are chained, in chunk order.
-static int pipeline_slots() {
-    const char *e = getenv("PT_WF_SLOTS");
-    const int k = e ? atoi(e) : 2;
-    return k < 1 ? 1 : (k > WaveWorkspace::MAX_SLOTS ? WaveWorkspace::MAX_SLOTS : k);
-}
-
+// Chunks in flight (Tuning::wf_slots): each has its own path state (slot) and
+// runs on its own stream, so one chunk's bounce/compaction kernels fill the
+// tails of the other's march kernels (and its memory-bound bounces overlap the
+// other's VALU-bound marches).  Only the reduces are chained, in chunk order.
 static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -866,10 +841,13 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
         }
         if (ws->fork) (void)hipEventDestroy(ws->fork);
         if (ws->reduced) (void)hipEventDestroy(ws->reduced);
-        ws->fork = ws->reduced = nullptr;
+        if (ws->done) (void)hipEventDestroy(ws->done);
+        ws->fork = ws->reduced = ws->done = nullptr;
+        ws->used = false;
         ws->device = dev;
     }
     if (!ws->fork && (e = hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ws->done && (e = hipEventCreateWithFlags(&ws->done, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
     for (int k = 0; k < slots - 1; k++) {
         if (!ws->side[k] && (e = hipStreamCreateWithFlags(&ws->side[k], hipStreamNonBlocking)) != hipSuccess) return e;
@@ -878,13 +856,8 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     return hipSuccess;
 }
 
-// Minimum sample chunks per frame (PT_WF_MIN_CHUNKS, read per render).
+// Chunks keep at least MIN_CHUNK_PATHS paths to fill the device (Tuning::wf_min_chunks).
 constexpr uint32_t MIN_CHUNK_PATHS = 1u << 21;
-static uint32_t min_chunks() {
-    const char *e = getenv("PT_WF_MIN_CHUNKS");
-    const long v = e ? atol(e) : 1;
-    return (uint32_t)(v < 1 ? 1 : (v > 4096 ? 4096 : v));
-}
 
 struct Slot {
     WfView v;
@@ -894,7 +867,8 @@ struct Slot {
 template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws, int fkind) {
-    const uint32_t cap_want = wf_cap_paths();
+    const Tuning &tu = ws->tune;
+    const uint32_t cap_want = (uint32_t)tu.wf_paths;
     // tile groups (only for frames beyond cap_want pixels), then sample chunks
     const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
     const uint32_t ntiles = P0.tile_count;
@@ -905,10 +879,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     if (ns > P0.spp) ns = P0.spp;
     {
         // A small frame (one rank's share of a multi-GPU frame) still gets at
-        // least min_chunks() sample chunks, so the pipelined slots overlap one
+        // least wf_min_chunks sample chunks, so the pipelined slots overlap one
         // chunk's short tail iterations with the next chunk's work; chunks
         // keep at least MIN_CHUNK_PATHS paths to fill the device.
-        const uint32_t mc = min_chunks();
+        const uint32_t mc = (uint32_t)tu.wf_min_chunks;
         if (mc > 1 && ntiles <= group_tiles) {
             uint32_t want = (P0.spp + mc - 1) / mc;
             const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;
@@ -922,10 +896,14 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const uint32_t cap_tiles = (cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
     // no more slots than chunks
     const uint64_t chunks = (uint64_t)((ntiles + group_tiles - 1) / group_tiles) * ((P0.spp + ns - 1) / ns);
-    int slots = pipeline_slots();
+    int slots = tu.wf_slots;
     if ((uint64_t)slots > chunks) slots = (int)chunks;
     hipError_t e = ensure_streams(ws, slots);
     if (e != hipSuccess) return e;
+    // One workspace serves every frame of the renderer, whichever stream it is
+    // queued on (render_start's own stream, a caller's stream in
+    // render_device): this frame's kernels wait for the previous frame's.
+    if (ws->used && (e = hipStreamWaitEvent(st, ws->done, 0)) != hipSuccess) return e;
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
     const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
     const size_t slot_bytes = al((size_t)cap * 8) * 11 + al((size_t)cap * 4) * 4 + al((size_t)cap * 4 * (P0.depth + 1)) +
@@ -970,33 +948,25 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     for (int k = 0; k < slots; k++) sl[k].v.acc = acc;
     if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
 
-    // persistent march grid: exactly the resident blocks of the device
-    static uint32_t march_blocks = [] {
-        int dev = 0, cus = 256, per = 3;
-        if (hipGetDevice(&dev) == hipSuccess) {
-            hipDeviceProp_t pr;
-            if (hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
-        }
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, wf_march<false, march::F_HEART>, 256, 0) ==
-                hipSuccess &&
-            occ > 0)
-            per = occ;
-        const char *e = getenv("PT_WF_MARCH_BLOCKS_PER_CU");  // tuning knob
-        if (e && atoi(e) > 0 && atoi(e) < per) per = atoi(e);
-        return (uint32_t)(cus * per);
-    }();
-    static uint32_t march_slice = [] {
-        const char *e = getenv("PT_WF_MARCH_SLICE");  // tuning knob: 0 = one contiguous slice per block (measured: 256 is 7 % faster)
-        return e ? (uint32_t)atoi(e) : 256u;
-    }();
+    // persistent march grid: exactly the resident blocks of the device (or
+    // Tuning::wf_march_blocks_per_cu per CU, if fewer)
+    static const uint32_t march_resident = resident_blocks(wf_march<false, march::F_HEART>);
+    uint32_t march_blocks = march_resident;
+    if (tu.wf_march_blocks_per_cu > 0) {
+        int dev = 0, cus = 256;
+        hipDeviceProp_t pr;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
+        const uint32_t want = (uint32_t)(cus * tu.wf_march_blocks_per_cu);
+        if (want < march_blocks) march_blocks = want;
+    }
+    const uint32_t march_slice = (uint32_t)tu.wf_march_slice;
     // the side streams start after everything the caller queued on st
     if (slots > 1) {
         if ((e = hipEventRecord(ws->fork, st)) != hipSuccess) return e;
         for (int k = 0; k < slots - 1; k++)
             if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
     }
-    const bool fused = fused_bounces() && !ws->diag;
+    const bool fused = tu.wf_fused && !ws->diag;
     uint64_t c = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
@@ -1018,15 +988,15 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if (bb > 8192) bb = 8192;
             // iteration 0: slots [0, paths) are the chunk's camera rays
             if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-            if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind);
-            else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind);
+            if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);
+            else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             for (int it = 0; it < iters; it++) {
                 if (it > 0) {
                     if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-                    if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind);
-                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind);
+                    if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind, (uint32_t)tu.wf_trace_slice);
+                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind, tu.wf_bounce_waves);
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 }
@@ -1063,6 +1033,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         if ((e = hipEventRecord(ws->join[k], ws->side[k])) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(st, ws->join[k], 0)) != hipSuccess) return e;
     }
+    if ((e = hipEventRecord(ws->done, st)) != hipSuccess) return e;
+    ws->used = true;
     return hipSuccess;
 }
 

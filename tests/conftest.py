@@ -49,3 +49,14 @@ def cornell_text():
 @pytest.fixture(scope="session")
 def spheres_text():
     return scene_text("spheres.json")
+
+
+def host_threads(cap=16):
+    """Oracle threads: the CPUs this process may run on, at most `cap` (the GPU
+    box shows the whole machine in os.cpu_count() but grants one GPU's share)."""
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(cap, n))

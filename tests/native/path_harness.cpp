@@ -23,7 +23,7 @@ struct Bundle {
 
 extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, uint64_t seed) {
     try {
-        Bundle *b = new Bundle;
+        Bundle *b = new Bundle();  // value-initialised: every dev::Scene field not set below is 0 (cancel: none)
         b->sc = scene_from_json(json, len, random_spheres != 0, seed);
         b->acc = build_accel(b->sc, b->sc.json_shapes);
         for (auto &s : b->sc.shapes) b->shapes.push_back(to_device(s));

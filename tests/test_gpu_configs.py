@@ -12,7 +12,6 @@ C-ABI (the bench measures c2; these are parity cases):
 import json
 import os
 import sys
-from contextlib import contextmanager
 from pathlib import Path
 
 import numpy as np
@@ -22,20 +21,6 @@ import oracle as O
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
-
-
-@contextmanager
-def env(**kw):
-    old = {k: os.environ.get(k) for k in kw}
-    os.environ.update({k: str(v) for k, v in kw.items()})
-    try:
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")
@@ -69,9 +54,9 @@ def test_c3_chunked_equals_unchunked(pt, cornell):
     w, h, spp = 3840, 2160, 2
     r = pt.HipRenderer(ps, depth=8)
     a = r.render(cam, pt.ImageParams(w, h), spp, seed=3)
-    with env(PT_WF_PATHS=1 << 22):  # 1M paths: tile groups of 4096 tiles, one sample per chunk
-        r2 = pt.HipRenderer(ps, depth=8)
-        b = r2.render(cam, pt.ImageParams(w, h), spp, seed=3)
+    r2 = pt.HipRenderer(ps, depth=8)
+    r2.set_option("wf_paths", 1 << 22)  # 4M paths: tile groups of 16384 tiles, one sample per chunk
+    b = r2.render(cam, pt.ImageParams(w, h), spp, seed=3)
     assert np.array_equal(a, b)
 
 

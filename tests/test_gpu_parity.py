@@ -81,9 +81,11 @@ def test_ray_color_bit_exact(pt, cornell):
         assert int(st_gpu[i]) == s, i
 
 
-def render_pair(pt, scenes, w, h, spp, depth, seed):
+def render_pair(pt, scenes, w, h, spp, depth, seed, **opts):
     ps, osc = scenes
     r = pt.HipRenderer(ps, depth=depth)
+    for k, v in opts.items():
+        r.set_option(k, v)
     cam = ps.camera()
     img = r.render(cam, pt.ImageParams(w, h), spp, seed=seed)
     ref = osc.render(w, h, spp, depth, seed)
@@ -189,26 +191,6 @@ def test_count_work_diagnostic(pt, cornell):
     assert cnt["test_march"] > 0 and cnt["march_tries"] > 0
 
 
-class _env:
-    """Temporarily set engine knobs (read by the library at every launch)."""
-
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        import os
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update({k: str(v) for k, v in self.kv.items()})
-
-    def __exit__(self, *a):
-        import os
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
 def test_engines_agree_with_oracle(pt, cornell):
     """Cornell has the ray-marched Heart, so the default engine is the
     wavefront one; the megakernel must give the same bits, and both the
@@ -217,8 +199,8 @@ def test_engines_agree_with_oracle(pt, cornell):
     r = pt.HipRenderer(ps, depth=8)
     cam, ip = ps.camera(), pt.ImageParams(80, 45)
     wave = r.render(cam, ip, 3, seed=21)
-    with _env(PT_ENGINE="mega"):
-        mega = r.render(cam, ip, 3, seed=21)
+    r.set_option("engine", 1)  # megakernel
+    mega = r.render(cam, ip, 3, seed=21)
     assert np.array_equal(wave, mega)
     check_image(wave, osc.render(80, 45, 3, 8, 21))
 
@@ -231,37 +213,36 @@ def test_fused_bounces_equal_per_bounce_launches(pt, cornell, spheres):
     ps, osc = cornell
     r = pt.HipRenderer(ps, depth=8)
     cam, ip = ps.camera(), pt.ImageParams(96, 54)
-    with _env(PT_ENGINE="wave"):
-        split = r.render(cam, ip, 4, seed=31)
-        with _env(PT_WF_FUSED=1):
-            fused = r.render(cam, ip, 4, seed=31)
-            assert np.array_equal(fused, split)
-            with _env(PT_WF_PATHS=256 * 3):
-                small = r.render(cam, ip, 4, seed=31)
-            assert np.array_equal(fused, small)
-            img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
-            check_image(img, ref)
+    r.set_option("engine", 2)  # wavefront
+    split = r.render(cam, ip, 4, seed=31)
+    r.set_option("wf_fused", 1)
+    fused = r.render(cam, ip, 4, seed=31)
+    assert np.array_equal(fused, split)
+    r.set_option("wf_paths", 256 * 3)
+    small = r.render(cam, ip, 4, seed=31)
+    assert np.array_equal(fused, small)
+    img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6, engine=2, wf_fused=1)
+    check_image(img, ref)
     check_image(fused, osc.render(96, 54, 4, 8, 31))
 
 
 def test_wavefront_chunks_and_tile_groups(pt, cornell):
     """A tiny path budget forces one-tile groups and one-sample chunks: the
     running per-pixel sums must still add samples in order."""
-    with _env(PT_WF_PATHS=300):
-        img, ref = render_pair(pt, cornell, 37, 21, 3, 8, seed=9)
+    img, ref = render_pair(pt, cornell, 37, 21, 3, 8, seed=9, wf_paths=300)
     check_image(img, ref)
-    with _env(PT_WF_PATHS=256 * 7):  # 7 tiles x 1 spp per chunk, ragged last group
-        img, ref = render_pair(pt, cornell, 70, 45, 2, 8, seed=10)
-    check_image(img, ref)
+    # 7 tiles x 1 spp per chunk, ragged last group; one slot and three slots in flight
+    for slots in (1, 3):
+        img, ref = render_pair(pt, cornell, 70, 45, 2, 8, seed=10, wf_paths=256 * 7, wf_slots=slots)
+        check_image(img, ref)
 
 
 def test_wavefront_deep_paths(pt, spheres, cornell):
     """Depth 50 (the bins' depth) through the wavefront engine: 32-word stacks."""
-    with _env(PT_ENGINE="wave"):
-        img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6)
-        check_image(img, ref)
-        img, ref = render_pair(pt, cornell, 24, 16, 2, 20, seed=6)
-        check_image(img, ref)
+    img, ref = render_pair(pt, spheres, 40, 24, 2, 50, seed=6, engine=2)
+    check_image(img, ref)
+    img, ref = render_pair(pt, cornell, 24, 16, 2, 20, seed=6, engine=2)
+    check_image(img, ref)
 
 
 def test_wavefront_shards(pt, cornell):
@@ -279,11 +260,11 @@ def test_wavefront_shards(pt, cornell):
     for rank in range(world):
         r.render_device(cam, w, h, spp, 8, rank, world, g.data_ptr() + rank * per * 256 * 3 * 8, stream)
     frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
-    torch.cuda.synchronize()  # stream handle 0 is the renderer's own stream
+    # render_device and unshard_device queue on the same (torch current) stream: ordered
     pt.unshard_device(g.data_ptr(), w, h, world, frame.data_ptr(), stream)
     torch.cuda.synchronize()
-    with _env(PT_ENGINE="mega"):
-        want = r.render(cam, pt.ImageParams(w, h), spp, seed=8)
+    r.set_option("engine", 1)  # megakernel
+    want = r.render(cam, pt.ImageParams(w, h), spp, seed=8)
     assert np.array_equal(frame.cpu().numpy().reshape(-1, 3), want)
 
 
@@ -354,8 +335,8 @@ def test_marched_functions_frame_and_hits(pt):
     img, ref = render_pair(pt, (ps, osc), 96, 54, 2, 8, seed=3)
     check_image(img, ref)
     r = pt.HipRenderer(ps, depth=8)
-    with _env(PT_ENGINE="mega"):
-        mega = r.render(ps.camera(), pt.ImageParams(96, 54), 2, seed=3)
+    r.set_option("engine", 1)  # megakernel
+    mega = r.render(ps.camera(), pt.ImageParams(96, 54), 2, seed=3)
     assert np.array_equal(mega, img)
     rng = np.random.default_rng(31)
     rays = []

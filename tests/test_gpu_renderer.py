@@ -1,0 +1,252 @@
+"""The Renderer trait through the C-ABI on the GPU, as the reference's GUI
+drives it (src/bin/main.rs:262-290):
+
+* progressive, non-blocking render_step (step_by_step.rs:101-121): bands of a
+  C2-size frame arrive while the rest is still rendering, and every band that
+  has arrived already equals the oracle for its rows;
+* stop_rendering (mod.rs:55) abandons a frame in flight quickly and leaves
+  the renderer usable; the GUI's 1 spp -> 100 spp restart sequence;
+* the display encode (main.rs:281-289) on the GPU equals the host encode and
+  the reference's formula, fused into render_step_rgba8;
+* several devices behind one renderer (pt_renderer_create_multi): the tile
+  deal, peer copies and un-interleave reproduce the one-device frame bit for
+  bit (rehearsed with a repeated ordinal on the one GPU of the box);
+* frames queued on different streams share the renderer's workspace safely.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import host_threads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cornell(pt, cornell_text):
+    return pt.Scene.from_json(cornell_text, seed=1), O.Scene(cornell_text, seed=1).use_bvh(True, 7)
+
+
+def reference_encode(rgb):
+    """src/bin/main.rs:281-289 in numpy: sqrt, f64::clamp (NaN passes), *256, `as u8` (NaN -> 0, saturating)."""
+    with np.errstate(invalid="ignore"):
+        v = np.sqrt(rgb)
+        v = np.where(v < 0.0, 0.0, v)
+        v = np.where(v > 0.999, 0.999, v)
+        s = v * 256.0
+        s = np.where(np.isnan(s), 0.0, s)
+    out = np.zeros((len(rgb), 4), np.uint8)
+    out[:, :3] = np.clip(np.floor(s), 0, 255).astype(np.uint8)
+    out[:, 3] = 255
+    return out
+
+
+def sampled_rows_check(osc, img, w, h, spp, rows, n=2048, seed=0):
+    """img rows `rows` against the oracle on n random pixels of those rows (bit-exact)."""
+    rng = np.random.default_rng(seed)
+    ys = rng.choice(rows, size=n)
+    xs = rng.integers(0, w, size=n)
+    px = np.unique((ys * w + xs).astype(np.uint32))
+    ref = osc.render(w, h, spp, 8, 1, pixels=px, threads=host_threads())
+    assert np.array_equal(img[px], ref), "band pixels differ from the oracle"
+
+
+def test_progressive_bands_arrive_before_the_frame_ends(pt, cornell):
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h, spp = 1920, 1080, 16
+    buf = np.full((w * h, 3), np.nan)
+    r.start_rendering(cam, pt.ImageParams(w, h), spp, seed=1)
+    partial = None
+    polls = 0
+    while True:
+        done = r.render_step(buf, blocking=False)
+        polls += 1
+        if done:
+            break
+        rows_in = ~np.isnan(buf.reshape(h, w, 3)[:, 0, 0])
+        if partial is None and rows_in.any() and not rows_in.all():
+            partial = (buf.copy(), np.nonzero(rows_in)[0])
+    assert polls > 1
+    assert partial is not None, "no poll saw some bands copied and others still rendering"
+    snap, rows = partial
+    # the band boundaries are tile rows: whole 16-row groups arrive together
+    assert len(rows) % 16 == 0 or rows[-1] == h - 1
+    sampled_rows_check(osc, snap, w, h, spp, rows)
+    assert np.all(np.isfinite(buf))
+    # the bands seen early are the final frame's rows
+    assert np.array_equal(snap[rows[0] * w:(rows[-1] + 1) * w], buf[rows[0] * w:(rows[-1] + 1) * w])
+
+
+def test_gui_restart_sequence_and_stop(pt, cornell):
+    """main.rs:262-276: stop_rendering + start_rendering at 1 spp (interactive), then 100 spp."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h = 1920, 1080
+    buf = np.zeros((w * h, 3))
+    # interactive pass: 1 spp, polled to the end
+    r.stop_rendering()  # a stop with nothing in flight is a no-op
+    r.start_rendering(cam, pt.ImageParams(w, h), 1, seed=1)
+    while not r.render_step(buf):
+        pass
+    sampled_rows_check(osc, buf, w, h, 1, np.arange(h), n=4096, seed=1)
+    # high-sampling pass: 100 spp, abandoned early by a stop (camera moved)
+    r.stop_rendering()
+    r.start_rendering(cam, pt.ImageParams(w, h), 100, seed=1)
+    t0 = time.perf_counter()
+    r.stop_rendering()
+    t_stop = time.perf_counter() - t0
+    with pytest.raises(pt.PtError):
+        r.render_step(buf)  # nothing in flight after a stop
+    # the same 100 spp frame to the end, for comparison of the stop time
+    r.start_rendering(cam, pt.ImageParams(w, h), 100, seed=1)
+    t0 = time.perf_counter()
+    while not r.render_step(buf):
+        pass
+    t_full = time.perf_counter() - t0
+    assert t_stop < 0.5 * t_full, (t_stop, t_full)
+    sampled_rows_check(osc, buf, w, h, 100, np.arange(h), n=1024, seed=2)
+
+
+def test_restart_replaces_frame_in_flight(pt, cornell):
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h = 320, 180
+    buf = np.zeros((w * h, 3))
+    r.start_rendering(cam, pt.ImageParams(w, h), 64, seed=1)
+    r.start_rendering(cam, pt.ImageParams(w, h), 4, seed=1)  # stops the first
+    assert r.render_step(buf, blocking=True)
+    ref = osc.render(w, h, 4, 8, 1, threads=host_threads())
+    assert np.array_equal(buf, ref)
+
+
+def test_display_encode_device_equals_host_and_reference(pt, cornell):
+    import torch
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    w, h = 96, 54
+    img = r.render(ps.camera(), pt.ImageParams(w, h), 4, seed=1)
+    assert np.array_equal(img, osc.render(w, h, 4, 8, 1, threads=host_threads()))
+    special = np.array([[0.0, -0.0, 1.0], [4.0, -1.0, np.nan], [np.inf, -np.inf, 0.998],
+                        [0.999 ** 2, 1e-300, 5e-324], [0.25, 0.5, 0.75]])
+    rgb = np.concatenate([img, special])
+    host = pt.encode_rgba8(rgb)
+    assert np.array_equal(host, reference_encode(rgb))
+    d_rgb = torch.from_numpy(rgb.copy()).cuda()
+    d_rgba = torch.zeros(len(rgb) * 4, dtype=torch.uint8, device="cuda")
+    pt.encode_rgba8_device(d_rgb.data_ptr(), len(rgb), d_rgba.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_rgba.cpu().numpy().reshape(-1, 4), host)
+
+
+def test_render_step_rgba8_fused_encode(pt, cornell, tmp_path):
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    w, h = 400, 225
+    rgba = np.zeros((w * h, 4), np.uint8)
+    rgb = np.zeros((w * h, 3))
+    r.start_rendering(ps.camera(), pt.ImageParams(w, h), 8, seed=1)
+    while not r.render_step_rgba8(rgba, rgb):
+        pass
+    assert np.array_equal(rgba, pt.encode_rgba8(rgb))
+    sampled_rows_check(osc, rgb, w, h, 8, np.arange(h), n=1024, seed=3)
+    # without the linear buffer (the GUI's frame only)
+    rgba2 = np.zeros_like(rgba)
+    r.start_rendering(ps.camera(), pt.ImageParams(w, h), 8, seed=1)
+    assert r.render_step_rgba8(rgba2, blocking=True)
+    assert np.array_equal(rgba2, rgba)
+    pt.write_png(tmp_path / "rendered.png", rgba, w, h)
+    assert (tmp_path / "rendered.png").stat().st_size > w * h * 4
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_renderer_matches_one_device(pt, cornell, devices):
+    import torch
+    ps, osc = cornell
+    w, h, spp = 200, 120, 3
+    cam = ps.camera()
+    one = pt.HipRenderer(ps, device=0, depth=8).render(cam, pt.ImageParams(w, h), spp, seed=1)
+    rm = pt.HipRenderer(ps, depth=8, devices=devices)
+    assert rm.num_devices == len(devices)
+    # progressive path (bands over all devices)
+    got = rm.render(cam, pt.ImageParams(w, h), spp, seed=1)
+    assert np.array_equal(got, one)
+    # device-resident frame on a caller stream
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        rm.render_frame_device(cam, w, h, spp, 1, frame.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(frame.view(-1, 3).cpu().numpy(), one)
+    ref = osc.render(w, h, spp, 8, 1, threads=host_threads())
+    assert np.array_equal(one, ref)
+
+
+def test_multi_device_progressive_stop(pt, cornell):
+    ps, _ = cornell
+    rm = pt.HipRenderer(ps, depth=8, devices=[0, 0])
+    cam = ps.camera()
+    rm.start_rendering(cam, pt.ImageParams(1920, 1080), 64, seed=1)
+    rm.stop_rendering()
+    buf = np.zeros((64 * 36, 3))
+    rm.start_rendering(cam, pt.ImageParams(64, 36), 2, seed=1)
+    assert rm.render_step(buf, blocking=True)
+    one = pt.HipRenderer(ps, device=0, depth=8).render(cam, pt.ImageParams(64, 36), 2, seed=1)
+    assert np.array_equal(buf, one)
+
+
+def test_frames_on_different_streams_share_the_workspace(pt, cornell):
+    """render_device on a side stream, then render() with no sync in
+    between: the second frame waits for the first one's use of the workspace."""
+    import torch
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h = 160, 90
+    ref4 = osc.render(w, h, 4, 8, 1, threads=host_threads())
+    ref2 = osc.render(w, h, 2, 8, 7, threads=host_threads())
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    side = torch.cuda.Stream()
+    r.render_device(cam, w, h, 4, 1, 0, 1, frame.data_ptr(), side.cuda_stream)
+    img = r.render(cam, pt.ImageParams(w, h), 2, seed=7)  # the renderer's own stream, no sync first
+    side.synchronize()
+    assert np.array_equal(img, ref2)
+    assert np.array_equal(frame.view(-1, 3).cpu().numpy(), ref4)
+    # and the other way round, two caller streams back to back
+    f2 = torch.zeros_like(frame)
+    s2 = torch.cuda.Stream()
+    r.render_device(cam, w, h, 4, 1, 0, 1, frame.data_ptr(), side.cuda_stream)
+    r.render_device(cam, w, h, 2, 7, 0, 1, f2.data_ptr(), s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.view(-1, 3).cpu().numpy(), ref4)
+    assert np.array_equal(f2.view(-1, 3).cpu().numpy(), ref2)
+
+
+def test_tuning_options(pt, cornell):
+    """The knobs are explicit per-renderer options (pt_renderer_set_option),
+    not environment reads at every launch; no setting changes the image."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    opts = r.options()
+    assert set(opts) == set(pt.OPTION_DEFAULTS)
+    cam, ip = ps.camera(), pt.ImageParams(64, 40)
+    base = r.render(cam, ip, 3, seed=4)
+    for name, value in [("wf_slots", 1), ("wf_slots", 4), ("wf_march_slice", 0), ("wf_bounce_waves", 2),
+                        ("wf_march_blocks_per_cu", 1), ("wf_min_chunks", 3), ("engine", 1), ("mega_waves", 2)]:
+        r.set_option(name, value)
+        assert r.get_option(name) == value
+        assert np.array_equal(r.render(cam, ip, 3, seed=4), base), (name, value)
+        r.set_option(name, pt.OPTION_DEFAULTS[name])
+    for bad in [("no_such_knob", 1), ("wf_slots", 0), ("wf_slots", 99), ("wf_bounce_waves", 7)]:
+        with pytest.raises(pt.PtError):
+            r.set_option(*bad)
+    r.start_rendering(cam, ip, 64, seed=4)
+    with pytest.raises(pt.PtError):
+        r.set_option("wf_slots", 1)  # not while a frame is in flight
+    r.stop_rendering()
+    assert np.array_equal(base, osc.render(64, 40, 3, 8, 4, threads=host_threads()))

@@ -116,7 +116,7 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(os.environ.get("PT_AMD_LIB", str(LIB_PATH)))  # PT_AMD_LIB: an alternate build (tuning)
+    L = C.CDLL(os.environ.get("PT_AMD_LIB") or str(LIB_PATH))  # PT_AMD_LIB: an alternate build (tuning)
     vp, d = C.c_void_p, C.POINTER(C.c_double)
     u32, u64, sz = C.c_uint32, C.c_uint64, C.c_size_t
     sig = {
@@ -164,7 +164,7 @@ def lib():
         "pt_version": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
-        if "PT_AMD_LIB" in os.environ and not hasattr(L, name):
+        if os.environ.get("PT_AMD_LIB") and not hasattr(L, name):
             continue  # an older alternate build (tuning comparisons)
         f = getattr(L, name)
         f.restype = res

@@ -133,7 +133,7 @@ PT_HD int64_t lin_init(double x, double c, Lin *L) {
     if (Rs > 0.0 ? A > hi : (Rs < 0.0 && A < lo)) return PT_MPROF(lin_fail_zone), 0;
     L->X = X;
     L->R = R;
-    L->u = 1.0 / sc;  // exact
+    L->u = ldexp(1.0, e - 52);  // 1 / sc, exactly (a power of two; no division)
     if (Rs == 0.0) return BIG;
     const double span = Rs > 0.0 ? hi - A : A - lo, step = fabs(Rs);
     if (span >= BIGD * step) return BIG;
@@ -202,7 +202,8 @@ PT_HD int64_t steps_in_range_lb(double t, double s, double start, double end, in
     const double dist = s > 0.0 ? end - t : t - start;
     if (!(dist >= 0.0)) return 0;
     const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
-    const double k = floor(dist / (fabs(s) + delta) * (1.0 - 1e-12)) - 1.0;
+    // the quotient through a polished reciprocal (a few ulp): far inside the 1e-12 shrink
+    const double k = floor(dist * approx_rcp(fabs(s) + delta) * (1.0 - 1e-12)) - 1.0;
     (void)lim;
     if (!(k >= 0.0)) return 1;
     return k + 1.0 >= (double)cap ? cap : (int64_t)k + 1;
@@ -217,7 +218,7 @@ PT_HD int64_t steps_exit_ub(double t, double s, double start, double end) {
     const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
     const double as = fabs(s);
     if (!(dist >= 0.0) || !(as > 2.0 * delta)) return BIG;
-    const double k = ceil(dist / (as - delta) * (1.0 + 1e-12)) + 2.0;
+    const double k = ceil(dist * approx_rcp(as - delta) * (1.0 + 1e-12)) + 2.0;  // reciprocal: see above
     return k >= BIGD ? BIG : (int64_t)k;
 }
 
@@ -473,19 +474,22 @@ PT_HD double poly_eval(const Poly &P, double j, double *dg) {
     return g;
 }
 
+// A heuristic only (it sizes the block; the proof decides what is skipped), so
+// it divides through the hardware reciprocal.
 PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
     double L = sgn * P.g[0], S = sgn * P.g[1], Q = sgn * P.g[2];
     if (L <= 0.0) return 1.0;
     double r;
     if (Q == 0.0) {
-        r = S < 0.0 ? L / -S : cap;
+        r = S < 0.0 ? L * approx_rcp(-S) : cap;
     } else {
         double disc = S * S - 4.0 * Q * L;
         if (disc < 0.0) {
             r = cap;  // no real root of the quadratic
         } else {
             double sq = sqrt(disc);
-            double r1 = (-S - sq) / (2.0 * Q), r2 = (-S + sq) / (2.0 * Q);
+            const double i2q = approx_rcp(2.0 * Q);
+            double r1 = (-S - sq) * i2q, r2 = (-S + sq) * i2q;
             double lo = fmin(r1, r2), hi = fmax(r1, r2);
             r = lo > 0.0 ? lo : (hi > 0.0 ? hi : cap);
         }
@@ -556,12 +560,11 @@ struct MarchState {
 enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2, M_GUARD = 3 };
 constexpr uint32_t MARCH_GUARD = 1u << 24;
 
-// Bound test and start of the march; false if the ray misses the bound.
+// Start of the march on a bound interval [start, end] already known
+// (intersect_bound, ray_marching.rs:27-31), object-space ray (o, d).
 template <int FK = F_ANY>
-PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, double oy, double oz, double dx,
-                       double dy, double dz, MarchState *m) {
-    double start, end;
-    if (!shape_bound_k<FK>(F, ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+PT_HD void march_start(const FParams &F, double step0, int passes, double ox, double oy, double oz, double dx,
+                       double dy, double dz, double start, double end, MarchState *m) {
     m->F = F;
     PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz);
     m->start = start;
@@ -581,6 +584,15 @@ PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, do
     m->iters = 0;
     m->adv = 0;
     m->lit = 0;
+}
+
+// Bound test and start of the march; false if the ray misses the bound.
+template <int FK = F_ANY>
+PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, double oy, double oz, double dx,
+                       double dy, double dz, MarchState *m) {
+    double start, end;
+    if (!shape_bound_k<FK>(F, ox, oy, oz, dx, dy, dz, &start, &end)) return false;
+    march_start<FK>(F, step0, passes, ox, oy, oz, dx, dy, dz, start, end, m);
     return true;
 }
 

@@ -54,6 +54,10 @@ struct WfView {
     double *rx, *ry, *rz;  // sample radiance of finished paths
     uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
     uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
+    // march jobs pre-selected by the bounce kernel (scenes with one ray-marched
+    // shape, PT_WF_PRESELECT): object-space ray and bound interval per slot,
+    // 64 B each (o, d, start, end); null when the march kernel selects itself
+    double2 *jo;
     uint32_t *cnt;  // per iteration: [0] live-list count, [1] march-queue count, [2..3] unused
     double *acc;    // running per-pixel sums (3 per pixel of the tile group)
     uint32_t cap;   // path slots
@@ -219,6 +223,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
+                if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
+                    double2 *j = v.jo + (size_t)id * 4;
+                    j[0] = make_double2(o.x, o.y);
+                    j[1] = make_double2(o.z, d.x);
+                    j[2] = make_double2(d.y, d.z);
+                    j[3] = make_double2(st, en);
+                }
             }
             PT_BSTAMP(2)
             v.ox[id] = ray.o.x;
@@ -332,6 +343,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
+                if (need_march && v.jo) {
+                    double2 *j = v.jo + (size_t)id * 4;
+                    j[0] = make_double2(o.x, o.y);
+                    j[1] = make_double2(o.z, d.x);
+                    j[2] = make_double2(d.y, d.z);
+                    j[3] = make_double2(st, en);
+                }
             }
             if (need_march) {
                 v.ox[id] = ray.o.x;
@@ -470,6 +488,12 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_UNITS
 #define PT_WF_UNITS 1
 #endif
+#ifndef PT_WF_PRESELECT
+#define PT_WF_PRESELECT 1  // bounce kernel hands the march its object-space ray and bound (one marched shape): C2 +9 % (iso march 340 -> 275 ms, bounce 248 -> 256)
+#endif
+#ifndef PT_WF_INLINE_ADV
+#define PT_WF_INLINE_ADV (PT_WF_VOTE == 0)  // a proven block's exact advance in the same trip (0: PT_ADV_ROUNDS per trip)
+#endif
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 4  // waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs, 20 B: 1273; 3: 1261)
 #endif
@@ -523,12 +547,39 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     __syncthreads();
     uint32_t q = threadIdx.x;
     bool have = q < per && pos(q) < count;
+    // one marched shape and jobs pre-selected by the bounce kernel: a job is
+    // its march alone (no select, no ray transform, no bound quadratic here)
+    const bool pre = v.jo != nullptr;
+    int s0 = 0, passes0 = 0;
+    double step0 = 0.0;
+    march::FParams F0{};
+    if (pre) {
+        s0 = dev::uniform_load(&sc.march[0]);
+        const DShape S = dev::uniform_shape(&sc.shapes[s0]);
+        F0 = dev::shape_params(S);
+        step0 = S.p[0];
+        passes0 = S.depth;
+    }
     MarchJob cur;
-    if (have) load_job(v, mq[pos(q)], &cur);
+    march::MarchState ms;
     bool marching = false;
     int km = 0, mshape = -1;
-    V3 inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
-    march::MarchState ms;
+    auto start_job = [&](uint32_t id) {
+        if (pre) {
+            cur.id = id;
+            cur.best = v.t[id];
+            cur.who = v.who[id];
+            const double2 *j = v.jo + (size_t)id * 4;
+            const double2 a = j[0], b = j[1], c = j[2], e = j[3];
+            march::march_start<FK>(F0, step0, passes0, a.x, a.y, b.x, b.y, c.x, c.y, e.x, e.y, &ms);
+            marching = true;
+            mshape = s0;
+        } else {
+            load_job(v, id, &cur);
+        }
+    };
+    if (have) start_job(mq[pos(q)]);
+    V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
     unsigned long long dtrips[16], dcyc[16], dlanes[4];
     if (DIAG) {
@@ -580,7 +631,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
             bool done = false;
             if (marching) {
-                const int st = march::march_iter<false, PT_WF_VOTE == 0, FK>(ms, &mst);
+                const int st = march::march_iter<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -590,6 +641,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                         cur.who = mshape;
                     }
                     marching = false;
+                    done = pre;  // the job's only shape
                 }
             } else {
                 // select: next marched shape whose bound is entered before `best`
@@ -613,8 +665,8 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 v.who[cur.id] = cur.who;
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
-                if (have) load_job(v, mq[pos(q)], &cur);
-                if (have) {
+                if (have) start_job(mq[pos(q)]);
+                if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
                 }
@@ -906,7 +958,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     if (ws->used && (e = hipStreamWaitEvent(st, ws->done, 0)) != hipSuccess) return e;
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
     const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
-    const size_t slot_bytes = al((size_t)cap * 8) * 11 + al((size_t)cap * 4) * 4 + al((size_t)cap * 4 * (P0.depth + 1)) +
+    // pre-selected march jobs: one marched shape, PT_WF_PRESELECT
+    const bool presel = PT_WF_PRESELECT && sc.nmarch == 1 && !ws->diag;
+    const size_t slot_bytes = al((size_t)cap * 8) * 11 + (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 4 +
+                              al((size_t)cap * 4 * (P0.depth + 1)) +
                               al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 8) + al(cnt_words * 4) +
                               al(att_bytes);
     const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
@@ -942,6 +997,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
         v.cnt = (uint32_t *)take(cnt_words * 4);
         v.att = att_bytes ? (double *)take(att_bytes) : nullptr;
+        v.jo = presel ? (double2 *)take((size_t)cap * 64) : nullptr;
         v.cap = cap;
     }
     double *acc = (double *)take((size_t)npix_max * 24);

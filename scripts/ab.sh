@@ -1,0 +1,33 @@
+#!/bin/bash
+# A/B bench of variant libraries on the GPU box:  bash scripts/ab.sh <tag> <reps> name1 name2 ...
+# ("default" = the in-tree library).  One bench line per (rep, variant) in gpurun_out/<tag>/ab.log.
+set -e
+tag=$1; reps=$2; shift 2
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$tag
+mkdir -p $OUT
+cd $R
+for rep in $(seq 1 $reps); do
+    for v in "$@"; do
+        if [ "$v" = default ]; then lib=""; else lib=$R/variants/$v.so; fi
+        echo "== $v rep $rep" >> $OUT/ab.log
+        PT_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --parity-pixels 64 --steps 3 ${BENCH_ARGS} \
+            >> $OUT/ab.log 2>&1
+    done
+done
+python3 - "$OUT/ab.log" > $OUT/ab_summary.txt <<'PY'
+import json, sys, collections
+vals = collections.defaultdict(list); cur = None
+for line in open(sys.argv[1]):
+    if line.startswith("== "):
+        cur = line.split()[1]
+    elif line.startswith("{"):
+        r = json.loads(line)
+        k = r["roofline"]["kernels"]
+        vals[cur].append((r["value"], r["exact_pixels_frac"], k.get("wf_march", {}).get("ms_per_frame"),
+                          k.get("wf_bounce", {}).get("ms_per_frame")))
+for v, xs in vals.items():
+    print("%-14s value %s  exact %s  iso march ms %s  iso bounce ms %s" % (v, [x[0] for x in xs], [x[1] for x in xs],
+          [x[2] for x in xs], [x[3] for x in xs]))
+PY
+cat $OUT/ab_summary.txt

@@ -2,13 +2,18 @@
 
 For world N, each rank r renders its round-robin tiles (render_device with
 rank r of N) into its compact shard; the N-GPU frame time is the slowest
-rank's (plus the gather).  Running every rank's share on the one GPU we have
-gives that time without the other GPUs:
+rank's plus the frame-end gather and un-interleave.  Running every rank's
+share on the one GPU we have gives the compute part without the other GPUs;
+the gather is modelled by a device-to-device copy of the gathered bytes
+(world * per-rank shard, 24 B per pixel slot) plus the unshard kernel, timed
+on the same GPU (an xGMI gather moves the same bytes over ~7 links at
+~150 GB/s each, so this is a lower bound on its cost, not a measurement):
 
     python scripts/rank_sim.py [--worlds 1,8] [--spp 256] [--reps 2]
 
-Prints one JSON line per world: max/mean rank ms and the projected strong
-scaling efficiency t1 / (N * max_rank_ms) (the driver measures the real one).
+Prints one JSON line per world: max/mean rank ms, the gather model's ms, and
+two projected strong-scaling efficiencies: compute-only t1 / (N * max_rank_ms)
+and with the modelled gather.  The driver's SCALE run measures the real one.
 """
 import argparse
 import json
@@ -61,10 +66,25 @@ def main():
         mx = max(ms)
         if world == 1:
             t1 = mx
+        gather_ms = 0.0
+        if world > 1:  # the frame-end gather (modelled as a local D2D copy) and the un-interleave
+            per = pt.shard_tiles(W, H, 0, world)
+            g = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda")
+            src = torch.zeros_like(g)
+            frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
+            for rep in range(a.reps + 1):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                g.copy_(src)
+                pt.unshard_device(g.data_ptr(), W, H, world, frame.data_ptr(), sp)
+                torch.cuda.synchronize()
+                if rep:
+                    gather_ms = min(gather_ms or 1e30, (time.perf_counter() - t) * 1e3)
         rec = {"world": world, "max_rank_ms": round(mx, 2), "mean_rank_ms": round(sum(ms) / len(ms), 2),
-               "msamples_s": round(W * H * spp / mx / 1e3, 1)}
+               "gather_model_ms": round(gather_ms, 3), "msamples_s": round(W * H * spp / (mx + gather_ms) / 1e3, 1)}
         if t1:
-            rec["projected_eff"] = round(t1 / (world * mx), 3)
+            rec["projected_eff_compute_only"] = round(t1 / (world * mx), 3)
+            rec["projected_eff_with_gather_model"] = round(t1 / (world * (mx + gather_ms)), 3)
         print(json.dumps(rec), flush=True)
 
 

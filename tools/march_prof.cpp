@@ -114,7 +114,7 @@ int main(int argc, char **argv) {
         dev::Scene v{};
         v.shapes = shapes.data();
         v.mats = mats.data();
-        v.nodes = acc.nodes.data();
+        v.nodes = acc.cnodes.data();
         v.leaf = acc.leaf.data();
         v.lin = acc.lin.data();
         v.march = acc.march.data();

@@ -100,6 +100,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--scene-seed", type=int, default=1)
     ap.add_argument("--slots", type=int, default=None, help="chunk streams in flight (renderer default: 2)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a renderer tuning option (pt_renderer_set_option), repeatable")
     ap.add_argument("--single-process", action="store_true",
                     help="N GPUs behind one renderer (pt_renderer_create_multi, peer-copy gather) instead of ranks")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of each CPU-baseline run")
@@ -248,6 +250,9 @@ def main():
         r = pt.HipRenderer(scene, device=local, depth=args.depth)
     if args.slots:
         r.set_option("wf_slots", args.slots)
+    for o in args.option:
+        k, v = o.split("=", 1)
+        r.set_option(k, int(v))
     slots = r.get_option("wf_slots")
     cam = scene.camera()
     W, H, spp = args.width, args.height, args.spp

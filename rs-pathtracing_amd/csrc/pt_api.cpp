@@ -835,9 +835,9 @@ int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(r->device()));
     HIP_TRY(hipStreamSynchronize(r->stream()));
-    if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 40 ? n : 40) * 8, hipMemcpyDeviceToHost));
-    if (enable && !r->gpus[0].ws.diag) HIP_TRY(hipMalloc(&r->gpus[0].ws.diag, 40 * 8));
-    if (r->gpus[0].ws.diag) HIP_TRY(hipMemset(r->gpus[0].ws.diag, 0, 40 * 8));
+    if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 48 ? n : 48) * 8, hipMemcpyDeviceToHost));
+    if (enable && !r->gpus[0].ws.diag) HIP_TRY(hipMalloc(&r->gpus[0].ws.diag, 48 * 8));
+    if (r->gpus[0].ws.diag) HIP_TRY(hipMemset(r->gpus[0].ws.diag, 0, 48 * 8));
     if (!enable && r->gpus[0].ws.diag) {
         HIP_TRY(hipFree(r->gpus[0].ws.diag));
         r->gpus[0].ws.diag = nullptr;

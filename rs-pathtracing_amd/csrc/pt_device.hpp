@@ -821,7 +821,7 @@ PT_HD V3 trace_pixel(const Scene &sc, const FrameParams &P, uint32_t x, uint32_t
         if (phase == PH_MARCH) {
             if (TIMING) pt->march_passes++;
             for (int it = 0; it < MARCH_ITERS; it++) {
-                int st = march::march_iter<STATS, true, FK>(ms, &mst);
+                int st = march::march_step<STATS, true, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) {
                         note_guard(sc.guard);

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void march_probe(const double *__restrict__ jo
     F.func = march::F_HEART;
     if (march::march_begin(F, j[0], (int)j[1], j[2], j[3], j[4], j[5], j[6], j[7], &m)) {
         march::MarchStats ms{0, 0, 0, 0};
-        while ((st = march::march_iter<false>(m, &ms)) == march::M_RUNNING) k++;
+        while ((st = march::march_step<false>(m, &ms)) == march::M_RUNNING) k++;
     }
     t_out[i] = m.t;
     status[i] = st == march::M_DONE ? 1 : (st == march::M_GUARD ? 2 : 0);

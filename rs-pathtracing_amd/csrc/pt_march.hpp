@@ -40,6 +40,9 @@
 #ifndef PT_MHOOK
 #define PT_MHOOK(what) ((void)0)
 #endif
+#ifndef PT_MSEG
+#define PT_MSEG(k) ((void)0)
+#endif
 #ifndef PT_MCAPTURE
 #define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz) ((void)0)
 #endif
@@ -397,6 +400,9 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 #ifndef PT_PREFIX_RES
 #define PT_PREFIX_RES 1.0
 #endif
+#ifndef PT_MAX_LEVELS
+#define PT_MAX_LEVELS 40  // de Casteljau halvings per prefix search
+#endif
 // Longest provable prefix of a block: the largest integer b <= B such that
 // sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither the
 // approx_equal stop nor a sign change can fire before step b).  One Bernstein
@@ -427,7 +433,7 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
     c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
     double lo = 0.0, len = 1.0, proven = 0.0;  // in units of B
     PT_MHOOK(lv_begin);
-    for (int level = 0; level < 40; level++) {
+    for (int level = 0; level < PT_MAX_LEVELS; level++) {
         PT_MPROF(evals);
         double mn = fmin(fmin(fmin(c[1], c[2]), fmin(c[3], c[4])), fmin(fmin(c[5], c[6]), c[0]));
         if (mn > margin) {
@@ -525,6 +531,10 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
 #ifndef PT_ADV_ROUNDS
 #define PT_ADV_ROUNDS 64  // binade-segment rounds per march_advance call
 #endif
+#ifndef PT_ADV_K
+#define PT_ADV_K 0  // > 0: march_iter_k with at most K advance rounds per iteration
+#endif
+
 #ifndef PT_EARLY_MISS
 #define PT_EARLY_MISS 1
 #endif
@@ -558,7 +568,10 @@ struct MarchState {
 // M_GUARD: the march was dropped by MARCH_GUARD (callers take it as a miss
 // and count it: pt_march_guard_drops).
 enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2, M_GUARD = 3 };
-constexpr uint32_t MARCH_GUARD = 1u << 24;
+#ifndef PT_MARCH_GUARD
+#define PT_MARCH_GUARD (1u << 24)
+#endif
+constexpr uint32_t MARCH_GUARD = PT_MARCH_GUARD;  // (lowered only in timing experiments)
 
 // Start of the march on a bound interval [start, end] already known
 // (intersect_bound, ray_marching.rs:27-31), object-space ray (o, d).
@@ -599,14 +612,14 @@ PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, do
 // One round of a proven block's exact advance: one binade segment for each
 // of t, px, py, pz that still has steps to go; when all are done the block's
 // end point is exact and f is evaluated there.
-template <int FK = F_ANY>
+template <int FK = F_ANY, int ROUNDS = PT_ADV_ROUNDS>
 PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
     PT_MHOOK(block_begin);
-    for (int round = 0; round < PT_ADV_ROUNDS; round++) {
-        if (m.na[0] > 0.0) seg_step(m.t, m.s, m.na[0]);
-        if (m.na[1] > 0.0) seg_step(m.px, cx, m.na[1]);
-        if (m.na[2] > 0.0) seg_step(m.py, cy, m.na[2]);
-        if (m.na[3] > 0.0) seg_step(m.pz, cz, m.na[3]);
+    for (int round = 0; round < ROUNDS; round++) {
+        if (m.na[0] > 0.0) PT_MSEG(0), seg_step(m.t, m.s, m.na[0]);
+        if (m.na[1] > 0.0) PT_MSEG(1), seg_step(m.px, cx, m.na[1]);
+        if (m.na[2] > 0.0) PT_MSEG(2), seg_step(m.py, cy, m.na[2]);
+        if (m.na[3] > 0.0) PT_MSEG(3), seg_step(m.pz, cz, m.na[3]);
         if (!(m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0)) break;
     }
     if (m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0) return;
@@ -713,6 +726,108 @@ literal:
     return M_RUNNING;
 }
 
+// march_iter with one instance of each code region, for SIMT lanes that run
+// different phases in the same pass: the proof, then the advance rounds (a
+// block proven now and a block resumed from an earlier iteration share them),
+// then the literal step.  At most K advance rounds per iteration, so a lane
+// whose coordinate walks many binades (across zero, say) takes a few more
+// iterations instead of holding every other lane of its wave through its
+// rounds.  The sequence of reference steps, and so every value, is
+// march_iter's.
+template <bool STATS, int K, int FK = F_ANY>
+PT_HD int march_iter_k(MarchState &m, MarchStats *st) {
+    PT_MPROF(iters);
+    if (m.pass >= m.passes) return M_DONE;
+    if (++m.iters > MARCH_GUARD) return M_GUARD;
+    const double s = m.s;
+    const double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
+    bool lit = false;
+    if (!m.adv) {
+        if (m.t > m.end || m.t < m.start) return M_MISS;
+        lit = true;
+        if (m.lit > 0) {
+            m.lit--;
+        } else if (m.r != 0.0) {
+            if (m.lim < 0) m.lim = steps_in_range_lb(m.t, s, m.start, m.end, (int64_t)1 << 24);
+            const int64_t bmax = m.lim;
+            if (bmax >= 2) {
+                Poly P;
+                func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
+                if (STATS) st->tries++;
+                const double sgn = m.r > 0.0 ? 1.0 : -1.0;
+                const double guess = poly_root_guess(P, sgn, (double)bmax);
+                if (guess >= PT_MIN_GUESS) {
+                    const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
+                    int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
+                    if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
+                    int64_t good = poly_prefix<FK>(m.F, P, B, sgn);
+                    if (ub < BIG && good >= ub) return M_MISS;
+                    good = good > bmax ? bmax : good;
+                    if (good >= 2) {
+                        m.na[0] = m.na[1] = m.na[2] = m.na[3] = (double)good;
+                        m.lim -= good;
+                        m.adv = 1;
+                        // a prefix that stopped short of B ends just before the
+                        // crossing: the literal step follows the advance
+                        m.lit = PT_FOLD_LIT && good < B ? 1 : 0;
+                        if (STATS) st->blocks++;
+                        lit = false;
+                    }
+                }
+            }
+        }
+    }
+    if (m.adv) {
+#pragma unroll 1
+        for (int round = 0; round < K; round++) {
+            if (m.na[0] > 0.0) PT_MSEG(0), seg_step(m.t, s, m.na[0]);
+            if (m.na[1] > 0.0) PT_MSEG(1), seg_step(m.px, cx, m.na[1]);
+            if (m.na[2] > 0.0) PT_MSEG(2), seg_step(m.py, cy, m.na[2]);
+            if (m.na[3] > 0.0) PT_MSEG(3), seg_step(m.pz, cz, m.na[3]);
+            if (!(m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0)) break;
+        }
+        if (m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0) return M_RUNNING;
+        m.adv = 0;
+        m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
+        // the folded literal step, when the range bound still covers it (else
+        // the next iteration takes it after its range check)
+        if (m.lit > 0 && m.lim >= 1) {
+            m.lit--;
+            lit = true;
+        }
+    }
+    if (!lit) return M_RUNNING;
+    // ---- one literal step (ray_marching.rs:37-51)
+    if (m.lim > 0) m.lim--;
+    m.t += s;
+    m.px += cx;
+    m.py += cy;
+    m.pz += cz;
+    const double next = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
+    if (STATS) st->steps++;
+    if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
+        m.pass = m.passes;
+        return M_DONE;
+    }
+    if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
+        m.s = s * -0.01;
+        m.r = next;
+        m.lim = -1;
+        m.lit = 0;
+        m.pass++;
+        return m.pass >= m.passes ? M_DONE : M_RUNNING;
+    }
+    m.r = next;
+    return M_RUNNING;
+}
+
+// The iteration the march loops use: march_iter_k when PT_ADV_K > 0.
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
+PT_HD int march_step(MarchState &m, MarchStats *st) {
+    if constexpr (PT_ADV_K > 0) return march_iter_k<STATS, PT_ADV_K, FK>(m, st);
+    return march_iter<STATS, INLINE_ADV, FK>(m, st);
+}
+
 // What the next march_iter call will do, for wave-level phase scheduling
 // (wf_march): MP_CHEAP = a literal step or the end of the march, MP_ADV = an
 // advance round of a proven block, MP_PROOF = build the polynomial and prove
@@ -735,7 +850,7 @@ PT_HD bool func_march(const FParams &F, double step0, int passes, double ox, dou
     MarchState m;
     if (!march_begin<FK>(F, step0, passes, ox, oy, oz, dx, dy, dz, &m)) return false;
     int status;
-    while ((status = march_iter<STATS, true, FK>(m, st)) == M_RUNNING) {
+    while ((status = march_step<STATS, true, FK>(m, st)) == M_RUNNING) {
     }
     if (status == M_GUARD) st->guard++;
     if (status != M_DONE) return false;

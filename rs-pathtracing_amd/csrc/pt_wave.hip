@@ -149,20 +149,23 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 #endif
 
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
-// DIAG: wave-level s_memtime cycles per section (load + shade, trace,
-// march pre-check, stores) summed into diag[36..39] (tuning only).
+// DIAG: wave-level s_memtime cycles per section, each section ended by a
+// full s_waitcnt so the memory waits it causes are charged to it (tuning
+// only): list load, state loads, shade, unwind, trace, march pre-check,
+// stores; summed into diag[36..42].
 template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
     const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
-    unsigned long long dsec[4] = {0, 0, 0, 0}, tst = 0;
-#define PT_BSTAMP(k)                                         \
-    if (DIAG) {                                              \
+    unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
+#define PT_BSTAMP(k)                                                \
+    if (DIAG) {                                                     \
+        __builtin_amdgcn_s_waitcnt(0);                              \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
-        dsec[k] += n_ - tst;                                 \
-        tst = n_;                                            \
+        dsec[k] += n_ - tst;                                        \
+        tst = n_;                                                   \
     }
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         if (DIAG) tst = __builtin_amdgcn_s_memtime();
@@ -187,32 +190,38 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 }
             } else {
                 id = v.list[i];
+                PT_BSTAMP(0)
                 ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
                 ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
                 rng.s = v.rng[id];
                 const uint32_t meta = v.meta[id];
+                const int who0 = v.who[id];
+                const double t0 = v.t[id];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 if (EXT) stk.vb = v.att + id;
+                PT_BSTAMP(1)
                 V3 leaf;
-                if (dev::shade<false, FK, EXT>(sc, v.who[id], v.t[id], ray, depth, stk, rng, P.s11, &leaf)) {
+                const bool ended = dev::shade<false, FK, EXT>(sc, who0, t0, ray, depth, stk, rng, P.s11, &leaf);
+                PT_BSTAMP(2)
+                if (ended) {
                     const V3 c = unwind_mem<EXT>(sc, stk, leaf);
                     v.rx[id] = c.x;
                     v.ry[id] = c.y;
                     v.rz[id] = c.z;
                     live = false;
                 }
+                PT_BSTAMP(3)
             }
         }
-        PT_BSTAMP(0)
         bool need_march = false;
         if (live) {
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
             dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
-            PT_BSTAMP(1)
+            PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
             // march kernel repeats this select and marches)
             for (int k = 0; k < sc.nmarch && !need_march; k++) {
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     j[3] = make_double2(st, en);
                 }
             }
-            PT_BSTAMP(2)
+            PT_BSTAMP(5)
             v.ox[id] = ray.o.x;
             v.oy[id] = ray.o.y;
             v.oz[id] = ray.o.z;
@@ -244,11 +253,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             v.meta[id] = depth | ((uint32_t)stk.n << 8);
         }
         if (i < count) v.status[id] = live ? (need_march ? 3u : 1u) : 0u;
-        PT_BSTAMP(3)
+        PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
     if (DIAG && (threadIdx.x & 63) == 0)
-        for (int k = 0; k < 4; k++) atomicAdd(&diag[36 + k], dsec[k]);
+        for (int k = 0; k < 7; k++) atomicAdd(&diag[36 + k], dsec[k]);
 }
 
 // Fused bounces (PT_WF_FUSED=1; measured slower, see fused_bounces()): a lane carries its path through as
@@ -491,6 +500,12 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #ifndef PT_WF_PRESELECT
 #define PT_WF_PRESELECT 1  // bounce kernel hands the march its object-space ray and bound (one marched shape): C2 +9 % (iso march 340 -> 275 ms, bounce 248 -> 256)
 #endif
+#ifndef PT_WF_BOUNCE_CAP
+#define PT_WF_BOUNCE_CAP 8192  // bounce grid (blocks) after the first iteration; threads loop over the live list
+#endif
+#ifndef PT_WF_STORE_LATE
+#define PT_WF_STORE_LATE 1  // march: a finished job's results are stored after the next job's loads have landed
+#endif
 #ifndef PT_WF_INLINE_ADV
 #define PT_WF_INLINE_ADV (PT_WF_VOTE == 0)  // a proven block's exact advance in the same trip (0: PT_ADV_ROUNDS per trip)
 #endif
@@ -564,7 +579,8 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     march::MarchState ms;
     bool marching = false;
     int km = 0, mshape = -1;
-    auto start_job = [&](uint32_t id) {
+    auto start_job = [&](uint32_t k) {  // k: queue position
+        const uint32_t id = mq[k];
         if (pre) {
             cur.id = id;
             cur.best = v.t[id];
@@ -578,7 +594,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             load_job(v, id, &cur);
         }
     };
-    if (have) start_job(mq[pos(q)]);
+    if (have) start_job(pos(q));
     V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
     unsigned long long dtrips[16], dcyc[16], dlanes[4];
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
             bool done = false;
             if (marching) {
-                const int st = march::march_iter<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
+                const int st = march::march_step<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -661,11 +677,23 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 done = !marching;
             }
             if (done) {
-                v.t[cur.id] = cur.best;
-                v.who[cur.id] = cur.who;
+                // vmcnt counts loads and stores in issue order: a store issued
+                // before the next job's loads makes the wait for those loads a
+                // wait for the store's completion too
+                const uint32_t fid = cur.id;
+                const double fbest = cur.best;
+                const int fwho = cur.who;
+                if (!PT_WF_STORE_LATE) {
+                    v.t[fid] = fbest;
+                    v.who[fid] = fwho;
+                }
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
-                if (have) start_job(mq[pos(q)]);
+                if (have) start_job(pos(q));
+                if (PT_WF_STORE_LATE) {
+                    v.t[fid] = fbest;
+                    v.who[fid] = fwho;
+                }
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
@@ -1041,7 +1069,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, cs);
             if (e != hipSuccess) return e;
             uint32_t bb = (paths + 255) / 256;
-            if (bb > 8192) bb = 8192;
+            if (bb > PT_WF_BOUNCE_CAP) bb = PT_WF_BOUNCE_CAP;
             // iteration 0: slots [0, paths) are the chunk's camera rays
             if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
             if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);

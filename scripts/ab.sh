@@ -15,19 +15,5 @@ for rep in $(seq 1 $reps); do
             >> $OUT/ab.log 2>&1
     done
 done
-python3 - "$OUT/ab.log" > $OUT/ab_summary.txt <<'PY'
-import json, sys, collections
-vals = collections.defaultdict(list); cur = None
-for line in open(sys.argv[1]):
-    if line.startswith("== "):
-        cur = line.split()[1]
-    elif line.startswith("{"):
-        r = json.loads(line)
-        k = r["roofline"]["kernels"]
-        vals[cur].append((r["value"], r["exact_pixels_frac"], k.get("wf_march", {}).get("ms_per_frame"),
-                          k.get("wf_bounce", {}).get("ms_per_frame")))
-for v, xs in vals.items():
-    print("%-14s value %s  exact %s  iso march ms %s  iso bounce ms %s" % (v, [x[0] for x in xs], [x[1] for x in xs],
-          [x[2] for x in xs], [x[3] for x in xs]))
-PY
+python3 scripts/ab_summary.py $OUT/ab.log > $OUT/ab_summary.txt
 cat $OUT/ab_summary.txt

@@ -11,6 +11,7 @@
 #   bash scripts/gpu.sh pmc      <tag> [bench args...]    FETCH_SIZE / WRITE_SIZE passes (separate runs)
 #                                                         -> <tag>/pmc_traffic.json (scripts/pmc_traffic.py)
 #   bash scripts/gpu.sh sq       <tag> [bench args...]    SQ instruction-mix and lane-activity pass
+#   bash scripts/gpu.sh stall    <tag> [bench args...]    wave-cycle split: active / waiting on memory / issue-stalled
 #   bash scripts/gpu.sh evidence <tag>                    tests, smoke, bench, kt (default and one-stream)
 set -e
 cmd=$1; tag=$2; shift 2 || true
@@ -33,7 +34,8 @@ bench)
 kt)
     prof --kernel-trace --stats --output-format csv -d $OUT/kt -o bench -- python3 $R/bench.py "$@" \
         > $OUT/kt.log 2>&1
-    python3 scripts/kt_summary.py $OUT/kt > $OUT/kt_summary.txt ;;
+    python3 scripts/kt_summary.py $OUT/kt > $OUT/kt_summary.txt
+    python3 scripts/kt_leg.py $OUT/kt/bench_kernel_trace.csv $(( ${KT_FRAMES:-5} )) > $OUT/kt_one_stream_frame.txt || true ;;
 pmc)
     prof --kernel-trace --output-format csv -d $OUT/fetch -o p --pmc FETCH_SIZE -- python3 $R/bench.py "$@" \
         > $OUT/fetch.log 2>&1
@@ -46,6 +48,11 @@ sq)
         SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVES \
         -- python3 $R/bench.py "$@" > $OUT/sq.log 2>&1
     python3 scripts/pmc_summary.py $OUT/sq > $OUT/sq_summary.txt ;;
+stall)
+    prof --kernel-trace --output-format csv -d $OUT/stall -o p --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
+        -- python3 $R/bench.py "$@" > $OUT/stall.log 2>&1
+    python3 scripts/pmc_summary.py $OUT/stall > $OUT/stall_summary.txt ;;
 evidence)
     bash scripts/gpu.sh tests $tag
     bash scripts/gpu.sh smoke $tag

@@ -17,8 +17,10 @@ r.render_device(cam, W, H, spp, 1, 0, 1, frame.data_ptr(), 0)
 torch.cuda.synchronize()
 d = pt.wave_diag(r, False)
 trips, cyc, lanes = d[:16], d[16:32], d[32:36]
-bsec = d[36:40]
-print("bounce sections (wave cycles): " + ", ".join("%s %.1f%%" % (n, 100 * x / max(1, sum(bsec))) for n, x in zip(["load+shade", "trace", "precheck", "store"], bsec)))
+bsec = d[36:43]
+print("bounce sections (wave cycles, each ended by a full wait): " + ", ".join(
+    "%s %.1f%%" % (n, 100 * x / max(1, sum(bsec)))
+    for n, x in zip(["list", "state", "shade", "unwind", "trace", "precheck", "store"], bsec)))
 names = ["cheap", "select", "adv", "proof"]
 tot_trips, tot_cyc = sum(trips), sum(cyc)
 print("total trips %d  cycles %.3g" % (tot_trips, tot_cyc))

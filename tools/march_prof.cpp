@@ -28,6 +28,8 @@ struct Prof {
 static Prof g_prof;
 #define PT_MPROF(f) (g_prof.f++)
 #define PT_MHOOK(what) hook_##what()
+static int g_it_seg[4];
+#define PT_MSEG(k) (g_it_seg[k]++)
 static unsigned long long g_adv0, g_lv0;
 static void hook_adv_begin();
 static void hook_adv_end();
@@ -46,15 +48,18 @@ static void hook_block_end();
 
 using namespace pt;
 
+static int g_it_adv[8], g_it_nadv, g_it_levels;
 static void hook_adv_begin() { g_adv0 = g_prof.advance_loops; }
 static void hook_adv_end() {
     long k = (long)(g_prof.advance_loops - g_adv0);
+    if (g_it_nadv < 8) g_it_adv[g_it_nadv++] = (int)k;
     g_hist_adv[k < 63 ? k : 63]++;
     if (k > g_block_max) g_block_max = (int)k;
 }
 static void hook_lv_begin() { g_lv0 = g_prof.evals; }
 static void hook_lv_end() {
     long k = (long)(g_prof.evals - g_lv0);
+    g_it_levels += (int)k;
     g_hist_levels[k < 63 ? k : 63]++;
 }
 static void hook_block_begin() { g_block_max = 0; }
@@ -192,7 +197,7 @@ int main(int argc, char **argv) {
             uint32_t tr0 = ms.tries;
             int stt;
             long guard = 0;
-            while ((stt = march::march_iter<true>(m, &ms)) == march::M_RUNNING) {
+            while ((stt = march::march_step<true>(m, &ms)) == march::M_RUNNING) {
                 if (++guard > 2000000) {
                     printf("RUNAWAY job %zu: step %.17g passes %d o %.17g %.17g %.17g d %.17g %.17g %.17g  t %.17g s %.17g pass %d lim %lld r %.17g\n",
                            i, q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], m.t, m.s, m.pass,
@@ -228,7 +233,7 @@ int main(int argc, char **argv) {
                 int stt = march::M_MISS;
                 double k = 0;
                 if (march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m))
-                    while ((stt = march::march_iter<false>(m, &st2)) == march::M_RUNNING) k++;
+                    while ((stt = march::march_step<false>(m, &st2)) == march::M_RUNNING) k++;
                 double rec[3] = {m.t, stt == march::M_DONE ? 1.0 : 0.0, k};
                 fwrite(rec, sizeof rec, 1, o);
             }
@@ -250,6 +255,160 @@ int main(int argc, char **argv) {
             if (hist[i]) printf(" %d:%d", i, hist[i]);
         printf("\n");
         return bad ? 1 : 0;
+    }
+    if (argc >= 3 && !strcmp(argv[1], "sim")) {
+        // SIMT cost model of wf_march: waves of 64 lanes refill from their
+        // share of the queue; a trip costs every code region any lane runs,
+        // loops at the max trip count over the lanes.
+        FILE *f = fopen(argv[2], "rb");
+        std::vector<Job> jobs;
+        Job j;
+        while (fread(&j, sizeof j, 1, f) == 1) jobs.push_back(j);
+        fclose(f);
+        const double C_BASE = 30, C_REFILL = 120, C_TRY = 320, C_LEVEL = 55, C_SEG = 55, C_LIT = 45;
+        struct It { unsigned char tr, lit, lv, adv[4]; };
+        std::vector<std::vector<It>> rec(jobs.size());
+        for (size_t i = 0; i < jobs.size(); i++) {
+            const Job &q = jobs[i];
+            march::MarchState m;
+            march::MarchStats ms{0, 0, 0, 0};
+            if (!march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m)) continue;
+            int stt;
+            do {
+                g_it_nadv = 0;
+                g_it_levels = 0;
+                for (int k = 0; k < 8; k++) g_it_adv[k] = 0;
+                for (int k = 0; k < 4; k++) g_it_seg[k] = 0;
+                uint32_t t0 = ms.tries, s0 = ms.steps;
+                stt = march::march_step<true>(m, &ms);
+                It it;
+                it.tr = ms.tries != t0;
+                it.lit = ms.steps != s0;
+                it.lv = (unsigned char)(g_it_levels < 255 ? g_it_levels : 255);
+                for (int k = 0; k < 4; k++) it.adv[k] = (unsigned char)(g_it_adv[k] + g_it_seg[k] < 255 ? g_it_adv[k] + g_it_seg[k] : 255);
+                rec[i].push_back(it);
+            } while (stt == march::M_RUNNING && rec[i].size() < 100000);
+        }
+        const int per_wave = argc > 3 ? atoi(argv[3]) : 512;
+        // policy: at most K advance segments per coordinate inline; the rest
+        // resumes R segments per coordinate per later iteration
+        const int KIN = argc > 4 ? atoi(argv[4]) : 1000, RR = argc > 5 ? atoi(argv[5]) : 1;
+        if (KIN < 1000) {
+            for (auto &R : rec) {
+                std::vector<It> out;
+                for (auto it : R) {
+                    int rem[4], mx = 0;
+                    for (int k = 0; k < 4; k++) { rem[k] = it.adv[k] > KIN ? it.adv[k] - KIN : 0; if (rem[k] > mx) mx = rem[k]; it.adv[k] = it.adv[k] > KIN ? KIN : it.adv[k]; }
+                    if (mx == 0) { out.push_back(it); continue; }
+                    bool lit = it.lit; it.lit = 0;  // the folded literal step moves to after the advance
+                    out.push_back(it);
+                    while (mx > 0) {
+                        It a{0, 0, 0, {0, 0, 0, 0}};
+                        mx = 0;
+                        for (int k = 0; k < 4; k++) { int d = rem[k] > RR ? RR : rem[k]; a.adv[k] = d; rem[k] -= d; if (rem[k] > mx) mx = rem[k]; }
+                        if (mx == 0) a.lit = lit;
+                        out.push_back(a);
+                    }
+                }
+                R.swap(out);
+            }
+        }
+        double tot = 0, useful = 0, wc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        long trips = 0;
+        for (size_t w0 = 0; w0 < jobs.size(); w0 += per_wave) {
+            size_t w1 = w0 + per_wave < jobs.size() ? w0 + per_wave : jobs.size();
+            size_t next = w0;
+            long lane_job[64], lane_pos[64];
+            for (int l = 0; l < 64; l++) {
+                lane_job[l] = next < w1 ? (long)next++ : -1;
+                lane_pos[l] = 0;
+            }
+            bool refill[64];
+            for (int l = 0; l < 64; l++) refill[l] = lane_job[l] >= 0;
+            for (;;) {
+                bool any = false, any_ref = false, any_try = false, any_lit = false;
+                int mlv = 0, madv[4] = {0, 0, 0, 0};
+                double lane_cost = 0;
+                for (int l = 0; l < 64; l++) {
+                    if (lane_job[l] < 0) continue;
+                    any = true;
+                    auto &R = rec[lane_job[l]];
+                    if (refill[l]) { any_ref = true; lane_cost += C_REFILL; refill[l] = false; }
+                    if (lane_pos[l] < (long)R.size()) {
+                        const It &it = R[lane_pos[l]];
+                        lane_cost += C_BASE + it.tr * C_TRY + it.lv * C_LEVEL + it.lit * C_LIT;
+                        any_try |= it.tr;
+                        any_lit |= it.lit;
+                        if (it.lv > mlv) mlv = it.lv;
+                        for (int k = 0; k < 4; k++) { lane_cost += it.adv[k] * C_SEG; if (it.adv[k] > madv[k]) madv[k] = it.adv[k]; }
+                        lane_pos[l]++;
+                    }
+                    if (lane_pos[l] >= (long)R.size()) {
+                        lane_job[l] = next < w1 ? (long)next++ : -1;
+                        lane_pos[l] = 0;
+                        refill[l] = lane_job[l] >= 0;
+                    }
+                }
+                if (!any) break;
+                double c = C_BASE + any_ref * C_REFILL + any_try * C_TRY + mlv * C_LEVEL + any_lit * C_LIT;
+                for (int k = 0; k < 4; k++) c += madv[k] * C_SEG;
+                wc[0] += C_BASE; wc[1] += any_ref * C_REFILL; wc[2] += any_try * C_TRY; wc[3] += mlv * C_LEVEL; wc[4] += any_lit * C_LIT;
+                for (int k = 0; k < 4; k++) wc[5] += madv[k] * C_SEG;
+                int act = 0; for (int l = 0; l < 64; l++) act += lane_job[l] >= 0; if (act < 16) wc[6] += c;
+                tot += c;
+                useful += lane_cost / 64.0;
+                trips++;
+            }
+        }
+        printf("jobs %zu trips %ld  wave cost %.4g  useful %.4g  lane utilisation %.1f / 64\n", jobs.size(), trips, tot,
+               useful, 64.0 * useful / tot);
+        printf("wave cost: base %.3g refill %.3g try %.3g levels %.3g literal %.3g advance %.3g  (trips with <16 lanes busy: %.3g)\n",
+               wc[0], wc[1], wc[2], wc[3], wc[4], wc[5], wc[6]);
+        // breakdown of lane work
+        double w_try = 0, w_lv = 0, w_adv = 0, w_lit = 0;
+        for (auto &R : rec) for (auto &it : R) { w_try += it.tr * C_TRY; w_lv += it.lv * C_LEVEL; w_lit += it.lit * C_LIT; for (int k = 0; k < 4; k++) w_adv += it.adv[k] * C_SEG; }
+        printf("lane work: try %.3g levels %.3g advance %.3g literal %.3g refill %.3g\n", w_try, w_lv, w_adv, w_lit, C_REFILL * jobs.size());
+        return 0;
+    }
+    if (argc >= 3 && !strcmp(argv[1], "tail")) {  // per-job detail of the longest marches
+        FILE *f = fopen(argv[2], "rb");
+        std::vector<Job> jobs;
+        Job j;
+        while (fread(&j, sizeof j, 1, f) == 1) jobs.push_back(j);
+        fclose(f);
+        const long thr = argc > 3 ? atol(argv[3]) : 40;
+        std::vector<long> hist(20, 0);
+        long long tot_it = 0, tail_it = 0;
+        for (size_t i = 0; i < jobs.size(); i++) {
+            const Job &q = jobs[i];
+            march::MarchState m;
+            march::MarchStats ms{0, 0, 0, 0};
+            if (!march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m)) continue;
+            long k = 0;
+            int stt;
+            unsigned long long ev0 = g_prof.evals, al0 = g_prof.advance_loops;
+            int pass_it[4] = {0, 0, 0, 0};
+            while ((stt = march::march_step<true>(m, &ms)) == march::M_RUNNING) {
+                k++;
+                if (m.pass < 4) pass_it[m.pass]++;
+            }
+            tot_it += k;
+            int b = 0;
+            while ((1l << b) <= k && b < 19) b++;
+            hist[b]++;
+            if (k >= thr) {
+                tail_it += k;
+                if (thr >= 0 && (long)i % 1 == 0)
+                    printf("job %zu iters %ld status %d steps %u tries %u blocks %u evals %llu advloops %llu per-pass %d %d %d  t %.6g s0 %g start %.6g end %.6g d %.3g %.3g %.3g o %.3g %.3g %.3g\n",
+                           i, k, stt, ms.steps, ms.tries, ms.blocks, g_prof.evals - ev0, g_prof.advance_loops - al0,
+                           pass_it[0], pass_it[1], pass_it[2], m.t, q.step, m.start, m.end, q.d[0], q.d[1], q.d[2],
+                           q.o[0], q.o[1], q.o[2]);
+            }
+        }
+        printf("iteration log2 histogram:");
+        for (int b = 0; b < 20; b++) if (hist[b]) printf(" <%ld:%ld", 1l << b, hist[b]);
+        printf("\ntotal iters %lld, in jobs >= %ld: %lld\n", tot_it, thr, tail_it);
+        return 0;
     }
     fprintf(stderr, "usage: march_prof capture <scene.json> <pixels> <spp> <jobs.bin> | run <jobs.bin> [n]\n");
     return 2;

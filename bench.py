@@ -214,9 +214,10 @@ def parity_pixels(args):
     return np.unique(np.concatenate([grid, row, col])).astype(np.uint32)
 
 
-def traffic_file(workload):
+def profile_file(name, workload):
+    """A committed PMC result (profiles/rN/<name>) of this workload, newest round first."""
     for rnd in ("r2", "r1"):
-        f = ROOT / "profiles" / rnd / "pmc_traffic_c2.json"
+        f = ROOT / "profiles" / rnd / name
         if f.exists():
             tr = json.loads(f.read_text())
             if tr.get("workload") == workload:
@@ -343,9 +344,18 @@ def main():
         if multi:  # kernel timing covers the first device: its tile share
             share = pt.shard_tiles(W, H, 0, args.gpus) / pt.shard_tiles(W, H, 0, 1)
         samples_share = samples_frame * share
-        f_kind = {"march": flops_per_sample(counts, MARCH_EVENTS),
-                  "bounce": flops_per_sample(counts, [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS]),
-                  "megakernel": F}
+        f_weights = {"march": flops_per_sample(counts, MARCH_EVENTS),
+                     "bounce": flops_per_sample(counts, [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS]),
+                     "megakernel": F}
+        workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
+        # algorithmic FLOPs per sample: from the f64 instruction counters of a committed PMC pass of this
+        # workload (scripts/pmc_flops.py) when there is one, else the event counts times FLOP_WEIGHTS
+        ff, fl = profile_file("pmc_flops_c2.json", workload)
+        f_kind = dict(f_weights)
+        if fl:
+            for k, v in fl["kinds"].items():
+                f_kind[k] = v["algorithmic_flops_per_sample"]
+            F = f_kind["bounce"] + f_kind["march"]
         kname = {"bounce": "wf_bounce", "march": "wf_march", "megakernel": "render_tiles"}
         src = kt_iso if kt_iso is not None else kt
         nfr = 1 if kt_iso is not None else args.steps
@@ -358,11 +368,11 @@ def main():
             if n_k:
                 a_k = f_kind[k] * samples_share * nfr / (ms_k / 1e3) / 1e12
                 per_kernel[kname[k]] = {"achieved": round(a_k, 4), "frac": round(a_k / FP64_PEAK_TFLOPS, 5),
-                                        "flops_per_sample": round(f_kind[k], 1), "launches": n_k // nfr,
+                                        "flops_per_sample": round(f_kind[k], 1),
+                                        "flops_per_sample_weights": round(f_weights[k], 1), "launches": n_k // nfr,
                                         "ms_per_frame": round(ms_k / nfr, 3),
                                         "kernel_ms_avg": round(ms_k / n_k, 4)}
         out_bytes = 24.0 * W * H * share
-        workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
         tuning = {k: v for k, v in r.options().items() if v != pt.OPTION_DEFAULTS.get(k)}
         rec = {
             "metric": metric_name(args), "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n_gpus,
@@ -383,6 +393,11 @@ def main():
                                       if kt_iso is not None else "timed steps (launches of two chunk streams overlap)"),
                          "kernels": per_kernel,
                          "flops_per_sample_total": round(F, 1),
+                         "flops_source": ("f64 instruction counters x mean active lanes, %s (scripts/pmc_flops.py); "
+                                          "event weights give %.1f FLOP/sample (%.2fx)"
+                                          % (ff.relative_to(ROOT), f_weights["bounce"] + f_weights["march"],
+                                             (f_weights["bounce"] + f_weights["march"]) / F) if fl else
+                                          "kernel event counters (pt_count_work) x FLOP_WEIGHTS"),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},
                          # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
@@ -401,7 +416,7 @@ def main():
             rec["tuning"] = tuning
         # roofline.traffic: HBM bytes per launch of the same kernel from the committed PMC passes of this
         # workload (scripts/pmc_traffic.py; bench.py cannot read PMC counters itself)
-        tf, tr = traffic_file(workload)
+        tf, tr = profile_file("pmc_traffic_c2.json", workload)
         if tr and world == 1 and not multi:
             kind = tr.get("kinds", {}).get(dom)
             if kind:

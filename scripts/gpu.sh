@@ -47,7 +47,9 @@ sq)
     prof --kernel-trace --output-format csv -d $OUT/sq -o p --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
         SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVES \
         -- python3 $R/bench.py "$@" > $OUT/sq.log 2>&1
-    python3 scripts/pmc_summary.py $OUT/sq > $OUT/sq_summary.txt ;;
+    python3 scripts/pmc_summary.py $OUT/sq > $OUT/sq_summary.txt
+    python3 scripts/pmc_flops.py $OUT/sq ${SQ_FRAMES:-2} ${SQ_SAMPLES:-530841600} $OUT/pmc_flops.json \
+        "${WORKLOAD:-cornell_box.json 1920x1080 256spp depth 8}" > /dev/null ;;
 stall)
     prof --kernel-trace --output-format csv -d $OUT/stall -o p --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \

@@ -44,3 +44,34 @@ def test_committed_c2_traffic_matches_bench_workload():
     for kind in ("bounce", "march"):
         k = rec["kinds"][kind]
         assert k["launches"] > 0 and k["traffic"] > 0
+
+
+def test_pmc_flops_lane_scaling(tmp_path):
+    """scripts/pmc_flops.py: wave-instruction counts x mean active lanes / samples."""
+    d = tmp_path / "sq"
+    d.mkdir()
+    b = "void pt::wf_bounce<4, false, 3, false, 0, false>(pt::dev::Scene)"
+    rows = [("SQ_INSTS_VALU_ADD_F64", 100.0), ("SQ_INSTS_VALU_MUL_F64", 50.0), ("SQ_INSTS_VALU_FMA_F64", 10.0),
+            ("SQ_INSTS_VALU_TRANS_F64", 2.0), ("SQ_THREAD_CYCLES_VALU", 3200.0), ("SQ_ACTIVE_INST_VALU", 100.0),
+            ("SQ_INSTS_VALU", 400.0)]
+    with open(d / "p_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for name, v in rows:
+            w.writerow({"Dispatch_Id": 0, "Kernel_Name": b, "Counter_Name": name, "Counter_Value": v})
+    out = tmp_path / "f.json"
+    subprocess.run([sys.executable, str(ROOT / "scripts" / "pmc_flops.py"), str(d), "2", "10", str(out), "wl"],
+                   check=True, capture_output=True)
+    k = json.loads(out.read_text())["kinds"]["bounce"]
+    assert k["mean_active_lanes"] == 32.0
+    # per frame 50 ADD, 25 MUL wave instructions x 32 lanes / 10 samples
+    assert k["algorithmic_flops_per_sample"] == (50 + 25) * 32 / 10
+    assert k["executed_flops_per_sample"] == (50 + 25 + 2 * 5 + 1) * 32 / 10
+
+
+def test_committed_c2_flops_match_bench_workload():
+    rec = json.loads((ROOT / "profiles" / "r2" / "pmc_flops_c2.json").read_text())
+    assert rec["workload"] == "cornell_box.json 1920x1080 256spp depth 8"
+    for kind in ("bounce", "march"):
+        k = rec["kinds"][kind]
+        assert 1 <= k["mean_active_lanes"] <= 64 and k["algorithmic_flops_per_sample"] > 0

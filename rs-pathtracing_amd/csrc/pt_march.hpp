@@ -43,6 +43,9 @@
 #ifndef PT_MSEG
 #define PT_MSEG(k) ((void)0)
 #endif
+#ifndef PT_MTRACE
+#define PT_MTRACE(guess, B, good, bmax) ((void)0)
+#endif
 #ifndef PT_MCAPTURE
 #define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz) ((void)0)
 #endif
@@ -397,6 +400,9 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 #ifndef PT_FOLD_LIT
 #define PT_FOLD_LIT 1
 #endif
+#ifndef PT_FOLD_MAX
+#define PT_FOLD_MAX 3  // literal steps an iteration may take when the predicted crossing is that close
+#endif
 #ifndef PT_PREFIX_RES
 #define PT_PREFIX_RES 1.0
 #endif
@@ -411,8 +417,15 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 // descends into it.  The margin is the one for the whole block (M and the
 // drift only grow with b), and the halving's own rounding (<= 24 levels of
 // exact-weight averages) stays far inside its 256 eps M part.
+#ifndef PT_TARGET_SPLIT
+#define PT_TARGET_SPLIT 1
+#endif
+#ifndef PT_EM_LEVELS
+#define PT_EM_LEVELS 40  // halvings of a failed early-miss proof (the next proof restarts from a fresh guess)
+#endif
 template <int FK>
-PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn) {
+PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn, int64_t target = 0,
+                          int max_levels = PT_MAX_LEVELS) {
     const double Bd = (double)B;
     const double margin = poly_margin<FK>(F, P, Bd);
     double a[7];
@@ -431,9 +444,35 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
     c[4] = a[0] + a[1] * (2.0 / 3.0) + a[2] * 0.4 + a[3] * 0.2 + a[4] * (1.0 / 15.0);
     c[5] = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
     c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
+    if (PT_TARGET_SPLIT && target >= 2 && target < B) {
+        // One split at the step just before the predicted crossing: de
+        // Casteljau at lambda >= target / B gives the control points of
+        // [0, lambda B], a superset of the steps [1, target]; if they clear
+        // the margin, target is the prefix and the halving search below is
+        // not needed.  lambda is target / B rounded up (an exact fma test),
+        // and the lerps' rounding (6 levels, weights in [0, 1]) stays inside
+        // the margin's 256 eps M part like the halvings' do.
+        const double td = (double)target;
+        double lam = td * approx_rcp(Bd);
+        if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
+        if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
+        if (fma(lam, Bd, -td) >= 0.0 && lam <= 1.0) {
+            double w[7];
+#pragma unroll
+            for (int i = 0; i < 7; i++) w[i] = c[i];
+            double mn = w[0];
+#pragma unroll
+            for (int r = 1; r < 7; r++) {
+#pragma unroll
+                for (int i = 0; i < 7 - r; i++) w[i] = w[i] + lam * (w[i + 1] - w[i]);
+                mn = fmin(mn, w[0]);
+            }
+            if (mn > margin) return target;
+        }
+    }
     double lo = 0.0, len = 1.0, proven = 0.0;  // in units of B
     PT_MHOOK(lv_begin);
-    for (int level = 0; level < PT_MAX_LEVELS; level++) {
+    for (int level = 0; level < max_levels; level++) {
         PT_MPROF(evals);
         double mn = fmin(fmin(fmin(c[1], c[2]), fmin(c[3], c[4])), fmin(fmin(c[5], c[6]), c[0]));
         if (mn > margin) {
@@ -633,6 +672,7 @@ PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
 template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
     PT_MPROF(iters);
+    int nlit = 1;
     if (m.pass >= m.passes) return M_DONE;
     // Every iteration takes >= 1 reference step; a march still running after
     // 2^24 of them is one the reference itself would not finish (a step below
@@ -664,14 +704,23 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             // longer than the crossing distance would drown the near part)
             const double sgn = m.r > 0.0 ? 1.0 : -1.0;
             const double guess = poly_root_guess(P, sgn, (double)bmax);
-            if (guess < PT_MIN_GUESS) goto literal;  // the crossing is the next step or two
+            if (guess < PT_MIN_GUESS) {
+                PT_MTRACE(guess, 0, 0, bmax);
+                // the crossing is the next step or two: up to PT_FOLD_MAX
+                // literal steps in this iteration
+                nlit = guess >= 1.0 ? PT_FOLD_MAX : 1;
+                goto literal;
+            }
             // No crossing predicted before the range end: try to prove every
             // step up to (an upper bound on) the one that leaves the range;
             // then nothing can stop this pass first and the march misses.
             const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
             int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
             if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
-            int64_t good = poly_prefix<FK>(m.F, P, B, sgn);
+            // the step just before the predicted crossing
+            const int64_t target = ub == BIG ? (int64_t)ceil(guess) - 1 : 0;
+            int64_t good = poly_prefix<FK>(m.F, P, B, sgn, target, ub == BIG ? PT_MAX_LEVELS : PT_EM_LEVELS);
+            PT_MTRACE(guess, B, good, bmax);
             if (ub < BIG && good >= ub) return M_MISS;
             good = good > bmax ? bmax : good;
             if (good >= 2) {
@@ -695,35 +744,43 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
                     // a prefix that stopped short of B ends just before the
                     // crossing: take that literal step in this iteration
-                    if (PT_FOLD_LIT && good < B && m.lim >= 1) goto literal;
+                    if (PT_FOLD_LIT && good < B && m.lim >= 1) {
+                        // more than one when the predicted crossing is past the first
+                        nlit = guess > (double)good + 1.0 ? PT_FOLD_MAX : 1;
+                        goto literal;
+                    }
                 }
                 return M_RUNNING;
             }
         }
     }
 literal:
-    // ---- one literal step (ray_marching.rs:37-51)
-    if (m.lim > 0) m.lim--;
-    m.t += s;
-    m.px += cx;
-    m.py += cy;
-    m.pz += cz;
-    double next = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
-    if (STATS) st->steps++;
-    if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
-        m.pass = m.passes;
-        return M_DONE;
-    }
-    if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
-        m.s = s * -0.01;
+    // ---- literal steps (ray_marching.rs:37-51): nlit of them while no
+    // crossing ends the pass; the range check before each step after the
+    // first is covered by lim >= 1
+    for (;;) {
+        if (m.lim > 0) m.lim--;
+        m.t += s;
+        m.px += cx;
+        m.py += cy;
+        m.pz += cz;
+        const double next = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
+        if (STATS) st->steps++;
+        if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
+            m.pass = m.passes;
+            return M_DONE;
+        }
+        if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
+            m.s = s * -0.01;
+            m.r = next;
+            m.lim = -1;
+            m.lit = 0;
+            m.pass++;
+            return m.pass >= m.passes ? M_DONE : M_RUNNING;
+        }
         m.r = next;
-        m.lim = -1;
-        m.lit = 0;
-        m.pass++;
-        return m.pass >= m.passes ? M_DONE : M_RUNNING;
+        if (PT_FOLD_MAX <= 1 || --nlit <= 0 || m.lim < 1) return M_RUNNING;
     }
-    m.r = next;
-    return M_RUNNING;
 }
 
 // march_iter with one instance of each code region, for SIMT lanes that run
@@ -760,7 +817,8 @@ PT_HD int march_iter_k(MarchState &m, MarchStats *st) {
                     const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
                     int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
                     if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
-                    int64_t good = poly_prefix<FK>(m.F, P, B, sgn);
+                    const int64_t target = ub == BIG ? (int64_t)ceil(guess) - 1 : 0;
+                    int64_t good = poly_prefix<FK>(m.F, P, B, sgn, target, ub == BIG ? PT_MAX_LEVELS : PT_EM_LEVELS);
                     if (ub < BIG && good >= ub) return M_MISS;
                     good = good > bmax ? bmax : good;
                     if (good >= 2) {

@@ -30,6 +30,9 @@ static Prof g_prof;
 #define PT_MHOOK(what) hook_##what()
 static int g_it_seg[4];
 #define PT_MSEG(k) (g_it_seg[k]++)
+static bool g_trace = false;
+#define PT_MTRACE(guess, B, good, bmax) \
+    do { if (g_trace) printf("  [try guess %.4g B %lld good %lld bmax %lld]", (double)(guess), (long long)(B), (long long)(good), (long long)(bmax)); } while (0)
 static unsigned long long g_adv0, g_lv0;
 static void hook_adv_begin();
 static void hook_adv_end();
@@ -255,6 +258,39 @@ int main(int argc, char **argv) {
             if (hist[i]) printf(" %d:%d", i, hist[i]);
         printf("\n");
         return bad ? 1 : 0;
+    }
+    if (argc >= 3 && !strcmp(argv[1], "trace")) {  // iteration-by-iteration log of hit jobs
+        FILE *f = fopen(argv[2], "rb");
+        std::vector<Job> jobs;
+        Job j;
+        while (fread(&j, sizeof j, 1, f) == 1) jobs.push_back(j);
+        fclose(f);
+        int shown = 0, want = argc > 3 ? atoi(argv[3]) : 10;
+        for (size_t i = 0; i < jobs.size() && shown < want; i++) {
+            const Job &q = jobs[i];
+            march::MarchState m;
+            march::MarchStats ms{0, 0, 0, 0};
+            if (!march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m)) continue;
+            march::MarchState m0 = m;
+            int stt;
+            int it = 0;
+            while ((stt = march::march_step<false>(m, &ms)) == march::M_RUNNING) it++;
+            if (stt != march::M_DONE) continue;
+            shown++;
+            printf("job %zu: %d iterations, t %.17g\n", i, it + 1, m.t);
+            m = m0;
+            g_trace = true;
+            do {
+                int pass = m.pass;
+                double t0 = m.t;
+                uint32_t st0 = ms.steps;
+                printf(" pass %d t %.10g lim %lld:", pass, t0, (long long)m.lim);
+                stt = march::march_step<true>(m, &ms);
+                printf(" -> t %.10g lit %u status %d\n", m.t, ms.steps - st0, stt);
+            } while (stt == march::M_RUNNING);
+            g_trace = false;
+        }
+        return 0;
     }
     if (argc >= 3 && !strcmp(argv[1], "sim")) {
         // SIMT cost model of wf_march: waves of 64 lanes refill from their

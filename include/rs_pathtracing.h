@@ -251,11 +251,13 @@ int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
 #define PT_KERNEL_KINDS 5
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
 
-/* Diagnostic of the wavefront march kernel: returns (and clears) the counters
- * accumulated since the last call into out[min(n, 40)] — trips and s_memtime
- * cycles per mix of lane phases (16 + 16), lanes per phase (4), then the
- * bounce kernel's cycles per section (load+shade, trace, pre-check, store) — and turns
- * the instrumented build on (enable = 1) or off. */
+/* Diagnostic of the wavefront kernels: returns (and clears) the counters
+ * accumulated since the last call into out[min(n, 48)] — the march kernel's
+ * trips and s_memtime cycles per mix of lane phases (16 + 16), lanes per
+ * phase (4), then the bounce kernel's cycles per section (list load, state
+ * loads, shade, unwind, trace, march pre-check, stores; each section ended by
+ * a full s_waitcnt, so the waits it causes are charged to it) — and turns the
+ * instrumented build on (enable = 1) or off. */
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
 
 /* Diagnostic: render the whole frame (depth <= 8) with a timing build of the

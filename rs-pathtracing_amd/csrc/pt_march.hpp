@@ -570,9 +570,6 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
 #ifndef PT_ADV_ROUNDS
 #define PT_ADV_ROUNDS 64  // binade-segment rounds per march_advance call
 #endif
-#ifndef PT_ADV_K
-#define PT_ADV_K 0  // > 0: march_iter_k with at most K advance rounds per iteration
-#endif
 
 #ifndef PT_EARLY_MISS
 #define PT_EARLY_MISS 1
@@ -783,106 +780,12 @@ literal:
     }
 }
 
-// march_iter with one instance of each code region, for SIMT lanes that run
-// different phases in the same pass: the proof, then the advance rounds (a
-// block proven now and a block resumed from an earlier iteration share them),
-// then the literal step.  At most K advance rounds per iteration, so a lane
-// whose coordinate walks many binades (across zero, say) takes a few more
-// iterations instead of holding every other lane of its wave through its
-// rounds.  The sequence of reference steps, and so every value, is
-// march_iter's.
-template <bool STATS, int K, int FK = F_ANY>
-PT_HD int march_iter_k(MarchState &m, MarchStats *st) {
-    PT_MPROF(iters);
-    if (m.pass >= m.passes) return M_DONE;
-    if (++m.iters > MARCH_GUARD) return M_GUARD;
-    const double s = m.s;
-    const double cx = m.dx * s, cy = m.dy * s, cz = m.dz * s;
-    bool lit = false;
-    if (!m.adv) {
-        if (m.t > m.end || m.t < m.start) return M_MISS;
-        lit = true;
-        if (m.lit > 0) {
-            m.lit--;
-        } else if (m.r != 0.0) {
-            if (m.lim < 0) m.lim = steps_in_range_lb(m.t, s, m.start, m.end, (int64_t)1 << 24);
-            const int64_t bmax = m.lim;
-            if (bmax >= 2) {
-                Poly P;
-                func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
-                if (STATS) st->tries++;
-                const double sgn = m.r > 0.0 ? 1.0 : -1.0;
-                const double guess = poly_root_guess(P, sgn, (double)bmax);
-                if (guess >= PT_MIN_GUESS) {
-                    const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
-                    int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
-                    if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
-                    const int64_t target = ub == BIG ? (int64_t)ceil(guess) - 1 : 0;
-                    int64_t good = poly_prefix<FK>(m.F, P, B, sgn, target, ub == BIG ? PT_MAX_LEVELS : PT_EM_LEVELS);
-                    if (ub < BIG && good >= ub) return M_MISS;
-                    good = good > bmax ? bmax : good;
-                    if (good >= 2) {
-                        m.na[0] = m.na[1] = m.na[2] = m.na[3] = (double)good;
-                        m.lim -= good;
-                        m.adv = 1;
-                        // a prefix that stopped short of B ends just before the
-                        // crossing: the literal step follows the advance
-                        m.lit = PT_FOLD_LIT && good < B ? 1 : 0;
-                        if (STATS) st->blocks++;
-                        lit = false;
-                    }
-                }
-            }
-        }
-    }
-    if (m.adv) {
-#pragma unroll 1
-        for (int round = 0; round < K; round++) {
-            if (m.na[0] > 0.0) PT_MSEG(0), seg_step(m.t, s, m.na[0]);
-            if (m.na[1] > 0.0) PT_MSEG(1), seg_step(m.px, cx, m.na[1]);
-            if (m.na[2] > 0.0) PT_MSEG(2), seg_step(m.py, cy, m.na[2]);
-            if (m.na[3] > 0.0) PT_MSEG(3), seg_step(m.pz, cz, m.na[3]);
-            if (!(m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0)) break;
-        }
-        if (m.na[0] > 0.0 || m.na[1] > 0.0 || m.na[2] > 0.0 || m.na[3] > 0.0) return M_RUNNING;
-        m.adv = 0;
-        m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
-        // the folded literal step, when the range bound still covers it (else
-        // the next iteration takes it after its range check)
-        if (m.lit > 0 && m.lim >= 1) {
-            m.lit--;
-            lit = true;
-        }
-    }
-    if (!lit) return M_RUNNING;
-    // ---- one literal step (ray_marching.rs:37-51)
-    if (m.lim > 0) m.lim--;
-    m.t += s;
-    m.px += cx;
-    m.py += cy;
-    m.pz += cz;
-    const double next = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
-    if (STATS) st->steps++;
-    if (fabs(next - 0.0) < 1e-15) {  // approx_equal(next, 0.0): break 'outer
-        m.pass = m.passes;
-        return M_DONE;
-    }
-    if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
-        m.s = s * -0.01;
-        m.r = next;
-        m.lim = -1;
-        m.lit = 0;
-        m.pass++;
-        return m.pass >= m.passes ? M_DONE : M_RUNNING;
-    }
-    m.r = next;
-    return M_RUNNING;
-}
-
-// The iteration the march loops use: march_iter_k when PT_ADV_K > 0.
+// The iteration the march loops use.  (Round 2 measured a variant with one
+// shared advance region and at most K binade segments per coordinate per
+// iteration, resumed in later iterations: slower for K = 2, 3, 4 and 64 —
+// DESIGN.md §3.2 — so a proven block's advance completes in its iteration.)
 template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
 PT_HD int march_step(MarchState &m, MarchStats *st) {
-    if constexpr (PT_ADV_K > 0) return march_iter_k<STATS, PT_ADV_K, FK>(m, st);
     return march_iter<STATS, INLINE_ADV, FK>(m, st);
 }
 

@@ -144,6 +144,9 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
     *y = ty * TILE + (((w >> 1) << 3) | (l >> 3));
 }
 
+#ifndef PT_WF_LONG_R2
+#define PT_WF_LONG_R2 1.1  // closest approach^2 to the marched shape's centre (object space) of a predicted-long job
+#endif
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
 #endif
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 PT_BSTAMP(3)
             }
         }
-        bool need_march = false;
+        bool need_march = false, long_job = false;
         if (live) {
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
@@ -238,6 +241,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     j[1] = make_double2(o.z, d.x);
                     j[2] = make_double2(d.y, d.z);
                     j[3] = make_double2(st, en);
+                    // queue order only: a ray passing within sqrt(PT_WF_LONG_R2) of the
+                    // shape's centre is likely to cross it (hits take ~3x the iterations)
+                    const double dd = dev::dot(d, d), od = dev::dot(o, d);
+                    long_job = dev::dot(o, o) - od * od / dd < PT_WF_LONG_R2;
                 }
             }
             PT_BSTAMP(5)
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             v.rng[id] = rng.s;
             v.meta[id] = depth | ((uint32_t)stk.n << 8);
         }
-        if (i < count) v.status[id] = live ? (need_march ? 3u : 1u) : 0u;
+        if (i < count) v.status[id] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
@@ -388,20 +395,25 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
 // counts (16 statuses per thread, one 16-byte load), one scan over the tile
 // counts, and an ordered scatter.  Neighbouring pixels stay in neighbouring
 // lanes, so the next kernels' structure-of-arrays loads stay coalesced and
-// march waves coherent.
+// march waves coherent.  March jobs the bounce kernel predicts long (bit 2:
+// the ray passes close to the marched shape's centre) go first in the queue,
+// each class in id order, so the persistent march grid's tail is made of
+// short jobs.
 constexpr int CP_ITEMS = 16, CP_BLOCK = 256, CP_TILE = CP_ITEMS * CP_BLOCK;
 
-__device__ __forceinline__ void cp_bits(uint4 q, uint32_t *live, uint32_t *march) {
-    // statuses are 0, 1 or 3: bit 0 of each byte = live, bit 1 = march
+__device__ __forceinline__ void cp_bits(uint4 q, uint32_t *live, uint32_t *march, uint32_t *lng) {
+    // statuses are 0, 1, 3 or 7: bit 0 of each byte = live, bit 1 = march, bit 2 = predicted long
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-    uint32_t l = 0, m = 0;
+    uint32_t l = 0, m = 0, g = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         l += __popc(w[k] & 0x01010101u);
         m += __popc(w[k] & 0x02020202u);
+        g += __popc(w[k] & 0x04040404u);
     }
     *live = l;
     *march = m;
+    *lng = g;
 }
 
 // block-wide exclusive scan of one value per thread (256 threads, 4 waves)
@@ -426,59 +438,69 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
     return before + inc - x;
 }
 
+// per tile: (live, long march, short march) counts in blk[3 * tile ..]
 __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk) {
-    __shared__ uint32_t lds[8];
+    __shared__ uint32_t lds[12];
     const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
-    uint32_t l, m, tl, tm;
-    cp_bits(q, &l, &m);
+    uint32_t l, m, g, tl, tg, ts;
+    cp_bits(q, &l, &m, &g);
     block_exscan(l, &tl, lds);
-    block_exscan(m, &tm, lds + 4);
+    block_exscan(g, &tg, lds + 4);
+    block_exscan(m - g, &ts, lds + 8);
     if (threadIdx.x == 0) {
-        blk[2 * blockIdx.x] = tl;
-        blk[2 * blockIdx.x + 1] = tm;
+        blk[3 * blockIdx.x] = tl;
+        blk[3 * blockIdx.x + 1] = tg;
+        blk[3 * blockIdx.x + 2] = ts;
     }
 }
 
-// one block: exclusive scan of the (live, march) tile counts in place; totals
-// go to the counters the next kernels read
+// one block: exclusive scan of the tile counts in place; totals go to the
+// counters the next kernels read (n_long: where the short march jobs start)
 __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, uint32_t *__restrict__ n_live,
-                                               uint32_t *__restrict__ n_march) {
-    __shared__ uint32_t lds[8];
-    uint32_t cl = 0, cm = 0;
+                                               uint32_t *__restrict__ n_march, uint32_t *__restrict__ n_long) {
+    __shared__ uint32_t lds[12];
+    uint32_t cl = 0, cg = 0, cs = 0;
     for (uint32_t b0 = 0; b0 < nblk; b0 += blockDim.x) {
         const uint32_t b = b0 + threadIdx.x;
-        const uint32_t l = b < nblk ? blk[2 * b] : 0u, m = b < nblk ? blk[2 * b + 1] : 0u;
-        uint32_t tl, tm;
-        const uint32_t el = block_exscan(l, &tl, lds), em = block_exscan(m, &tm, lds + 4);
+        const uint32_t l = b < nblk ? blk[3 * b] : 0u, g = b < nblk ? blk[3 * b + 1] : 0u,
+                       h = b < nblk ? blk[3 * b + 2] : 0u;
+        uint32_t tl, tg, ts;
+        const uint32_t el = block_exscan(l, &tl, lds), eg = block_exscan(g, &tg, lds + 4),
+                       es = block_exscan(h, &ts, lds + 8);
         if (b < nblk) {
-            blk[2 * b] = cl + el;
-            blk[2 * b + 1] = cm + em;
+            blk[3 * b] = cl + el;
+            blk[3 * b + 1] = cg + eg;
+            blk[3 * b + 2] = cs + es;
         }
         cl += tl;
-        cm += tm;
+        cg += tg;
+        cs += ts;
     }
     if (threadIdx.x == 0) {
         *n_live = cl;
-        *n_march = cm;
+        *n_march = cg + cs;
+        *n_long = cg;
     }
 }
 
 __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st, const uint32_t *__restrict__ blk,
-                                                  uint32_t *__restrict__ live_out, uint32_t *__restrict__ march_out) {
-    __shared__ uint32_t lds[8];
+                                                  const uint32_t *__restrict__ n_long, uint32_t *__restrict__ live_out,
+                                                  uint32_t *__restrict__ march_out) {
+    __shared__ uint32_t lds[12];
     const size_t base = (size_t)blockIdx.x * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
     const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
-    uint32_t l, m, tl, tm;
-    cp_bits(q, &l, &m);
-    uint32_t ol = blk[2 * blockIdx.x] + block_exscan(l, &tl, lds);
-    uint32_t om = blk[2 * blockIdx.x + 1] + block_exscan(m, &tm, lds + 4);
+    uint32_t l, m, g, tl, tg, ts;
+    cp_bits(q, &l, &m, &g);
+    uint32_t ol = blk[3 * blockIdx.x] + block_exscan(l, &tl, lds);
+    uint32_t og = blk[3 * blockIdx.x + 1] + block_exscan(g, &tg, lds + 4);
+    uint32_t os = *n_long + blk[3 * blockIdx.x + 2] + block_exscan(m - g, &ts, lds + 8);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int k = 0; k < CP_ITEMS; k++) {
         const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
         const uint32_t id = (uint32_t)(base + k);
         if (b & 1u) live_out[ol++] = id;
-        if (b & 2u) march_out[om++] = id;
+        if (b & 2u) march_out[(b & 4u) ? og++ : os++] = id;
     }
 }
 
@@ -990,7 +1012,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const bool presel = PT_WF_PRESELECT && sc.nmarch == 1 && !ws->diag;
     const size_t slot_bytes = al((size_t)cap * 8) * 11 + (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 4 +
                               al((size_t)cap * 4 * (P0.depth + 1)) +
-                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 8) + al(cnt_words * 4) +
+                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 12) + al(cnt_words * 4) +
                               al(att_bytes);
     const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
     e = reserve(ws, bytes);
@@ -1022,7 +1044,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         v.list = (uint32_t *)take((size_t)cap * 4);
         v.mq = (uint32_t *)take((size_t)cap * 4);
         v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
-        sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 8);
+        sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 12);
         v.cnt = (uint32_t *)take(cnt_words * 4);
         v.att = att_bytes ? (double *)take(att_bytes) : nullptr;
         v.jo = presel ? (double2 *)take((size_t)cap * 64) : nullptr;
@@ -1089,8 +1111,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
                 cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk);
-                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1]);
-                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, v.list, v.mq);
+                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
+                                                &v.cnt[it * 4 + 2]);
+                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;

@@ -291,6 +291,7 @@ struct Scene {
     const DImage *__restrict__ images;
     const uint8_t *__restrict__ pixels;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
+    int nmats;
     int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
     // marches dropped by the march guard (pt_march.hpp MARCH_GUARD), counted
     // on the device (pt_march_guard_drops); null: not counted

@@ -241,6 +241,7 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.nnodes = s.nnodes;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
+    d.nmats = s.nmats;
     d.diag = s.diag;
     d.guard = s.guard;
     return d;

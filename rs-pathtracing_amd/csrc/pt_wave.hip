@@ -128,6 +128,17 @@ __device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3
     return c;
 }
 
+// A path that ends stores its leaf radiance (emitted light, background or 0)
+// and its attenuation-stack depth; the per-pixel reduce unwinds the stack
+// (the recursion's products, in its order) when it sums the chunk's samples,
+// so the bounce kernel's waves never wait for the unwind's dependent loads.
+__device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const MemStack &stk, V3 leaf) {
+    v.rx[id] = leaf.x;
+    v.ry[id] = leaf.y;
+    v.rz[id] = leaf.z;
+    v.meta[id] = (uint32_t)stk.n << 8;
+}
+
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
 // thread-in-tile laid out as render_tiles' 4 waves of 8x8.
 __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v, uint32_t id, uint32_t *x,
@@ -209,10 +220,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const bool ended = dev::shade<false, FK, EXT>(sc, who0, t0, ray, depth, stk, rng, P.s11, &leaf);
                 PT_BSTAMP(2)
                 if (ended) {
-                    const V3 c = unwind_mem<EXT>(sc, stk, leaf);
-                    v.rx[id] = c.x;
-                    v.ry[id] = c.y;
-                    v.rz[id] = c.z;
+                    // the leaf radiance and the stack depth; wf_reduce unwinds
+                    // the attenuation stack (end_path)
+                    end_path(v, id, stk, leaf);
                     live = false;
                 }
                 PT_BSTAMP(3)
@@ -337,10 +347,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
         if (!done && shade_now) {
             V3 leaf;
             if (dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf)) {
-                const V3 c = unwind_mem<EXT>(sc, stk, leaf);
-                v.rx[id] = c.x;
-                v.ry[id] = c.y;
-                v.rz[id] = c.z;
+                end_path(v, id, stk, leaf);
                 v.status[id] = 0;
                 done = true;
             }
@@ -738,7 +745,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
 }
 
 // In-order per-pixel sum of the chunk's samples; mean after the last chunk.
-__global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int first, int last,
+// Each sample's radiance is first unwound from its path's end: the leaf
+// radiance times the attenuations its stack holds, in the recursion's order
+// (dev::unwind; end_path left the leaf and the stack depth).  Sample by
+// sample: a version unwinding 8 samples level by level together needs more
+// registers and measured slower (the kernel is latency-bound: occupancy wins).
+template <bool EXT>
+__global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, WfView v, int first, int last,
                                                  double *__restrict__ out) {
     const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
     if (pl >= v.npix) return;
@@ -756,7 +769,8 @@ __global__ __launch_bounds__(256) void wf_reduce(FrameParams P, WfView v, int fi
     V3 a = first ? dev::v3(0.0, 0.0, 0.0) : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
     for (uint32_t s = 0; s < v.ns; s++) {
         const size_t id = (size_t)s * v.npix + pl;
-        a = dev::add(a, dev::v3(v.rx[id], v.ry[id], v.rz[id]));
+        MemStack stk{v.ids + id, (size_t)v.cap, (int)(v.meta[id] >> 8), EXT ? v.att + id : nullptr};
+        a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(v.rx[id], v.ry[id], v.rz[id])));
     }
     if (last) {
         const V3 c = dev::divs(a, (double)P.spp);
@@ -1129,7 +1143,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             // the per-pixel sums take the chunks in order
             if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
-            wf_reduce<<<(v.npix + 255) / 256, 256, 0, cs>>>(P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+            if (sc.ext)
+                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+            else
+                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;

@@ -151,27 +151,61 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
     return (L.X + (double)j * L.R) * L.u;
 }
 
+// lin_init as straight-line code for SIMT lanes: every quantity is computed,
+// the cases are selects, and the room comes back as an exact f64 integer
+// (0: the closed form does not apply here; BIGD: unbounded).  The same room and
+// the same (X, R, u) wherever lin_init's room is >= 2, which is all its callers
+// use.  floor(span / step) needs one correction each way: span / step < 2^41
+// and the polished reciprocal is good to a few ulp, so the estimate is off by
+// less than 1.
+PT_HD double lin_room(double x, double c, Lin *L) {
+    PT_MPROF(lin_init);
+    const double ax = fabs(x), ac = fabs(c);
+    const bool ok0 = x != 0.0 && ax < 1e300 && ac < 1e300;  // zero, inf, NaN: no
+    const int e = ilogb(ok0 ? x : 1.0);
+    const double sc = ldexp(1.0, 52 - e);  // 1/u, a power of two: scaling by it is exact
+    const double q = c * sc, X = x * sc, aq = fabs(q);
+    const double qf = floor(q);
+    const bool tie = q - qf == 0.5;  // round-half-even: only from an even X (then R is the even neighbour)
+    const bool xodd = floor(X * 0.5) * 2.0 != X;
+    const double R = tie ? (floor(qf * 0.5) * 2.0 == qf ? qf : qf + 1.0) : rint(q);
+    const double C = ceil(aq);
+    const double lo = 4503599627370496.0 + C + 1.0, hi = 9007199254740992.0 - C - 1.0;
+    const double A = fabs(X), Rs = X >= 0.0 ? R : -R;
+    const bool zone = Rs > 0.0 ? A > hi : (Rs < 0.0 && A < lo);
+    const bool ok = ok0 && e >= -960 && aq < 4.0e15 && !(tie && xodd) && !zone;
+    L->X = X;
+    L->R = R;
+    L->u = ldexp(1.0, e - 52);
+    L->frozen = c == 0.0;
+    const double span = Rs > 0.0 ? hi - A : A - lo, step = fabs(Rs);
+    double k = floor(span * approx_rcp(step));
+    k = k * step > span ? k - 1.0 : k;
+    k = (k + 1.0) * step <= span ? k + 1.0 : k;
+    const double room = Rs == 0.0 || span >= BIGD * step ? BIGD : k + 1.0;
+    if (c == 0.0) return BIGD;
+    return ok ? room : 0.0;
+}
+
 // x after n literal additions fl(x + c), exactly, across any number of binade
 // edges: closed form inside each binade, literal adds in the thin zone at an
 // edge (and near zero).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
-PT_HD double advance(double x, double c, int64_t n) {
+PT_HD double advance(double x, double c, int64_t n_) {
     PT_MHOOK(adv_begin);
-    while (n > 0) {
+    double n = (double)n_;
+    while (n > 0.0) {
         PT_MPROF(advance_loops);
         Lin L;
-        int64_t room = lin_init(x, c, &L);
-        if (room >= 2) {
-            int64_t k = room < n ? room : n;
-            x = lin_at(L, x, k);
-            n -= k;
-            if (n > 0 && k == room) {  // the add that leaves the segment: literal
-                x = x + c;
-                n--;
-            }
-        } else {
+        const double room = lin_room(x, c, &L);
+        // the closed form to the end of the segment (or n), then the literal
+        // add that leaves it; a literal add alone in an edge zone
+        const double k = room >= 2.0 ? (room < n ? room : n) : 0.0;
+        if (k > 0.0) x = L.frozen ? x : (L.X + k * L.R) * L.u;
+        n -= k;
+        if (n > 0.0 && k == (room >= 2.0 ? room : 0.0)) {
             x = x + c;
-            n--;
+            n -= 1.0;
         }
     }
     PT_MHOOK(adv_end);
@@ -182,16 +216,11 @@ PT_HD double advance(double x, double c, int64_t n) {
 // (and the literal add leaving it), or one literal add in an edge zone.
 PT_HD void seg_step(double &x, double c, double &n) {
     Lin L;
-    const int64_t room = lin_init(x, c, &L);
-    if (room >= 2) {
-        const double k = (double)room < n ? (double)room : n;
-        x = lin_at(L, x, (int64_t)k);
-        n -= k;
-        if (n > 0.0 && k == (double)room) {
-            x = x + c;
-            n -= 1.0;
-        }
-    } else {
+    const double room = lin_room(x, c, &L);
+    const double k = room >= 2.0 ? (room < n ? room : n) : 0.0;
+    if (k > 0.0) x = L.frozen ? x : (L.X + k * L.R) * L.u;
+    n -= k;
+    if (n > 0.0 && k == (room >= 2.0 ? room : 0.0)) {
         x = x + c;
         n -= 1.0;
     }

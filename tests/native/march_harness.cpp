@@ -21,3 +21,65 @@ extern "C" int march_heart(double step, int passes, const double *inv /*3x4 row-
     steps[1] = st.tries;
     return hit;
 }
+
+// lin_room (the straight-line form the kernels use) against lin_init (the
+// branchy original) on n pseudo-random (x, c) pairs: the same room and the
+// same (X, R, u) wherever lin_init's room is >= 2, a room < 2 elsewhere.
+// Returns the number of disagreements.
+extern "C" long lin_room_check(long n, uint64_t seed) {
+    using namespace pt::march;
+    uint64_t s = seed;
+    auto next = [&s]() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto unit = [&]() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0; };
+    long bad = 0;
+    for (long i = 0; i < n; i++) {
+        const int mode = (int)(i % 6);
+        double x = unit() * ldexp(1.0, (int)(next() % 40) - 20);
+        double c = unit() * ldexp(1.0, (int)(next() % 60) - 50);
+        if (mode == 1) x = ldexp(1.0, (int)(next() % 20) - 10) * (1.0 + 1e-15 * (double)(next() % 8));  // binade edges
+        if (mode == 2) c = ldexp((double)(next() % 8) + 0.5, (int)(next() % 10) - 57);                  // ties
+        if (mode == 3) c = 0.0;
+        if (mode == 4) x = -x;
+        Lin A, B;
+        const int64_t ra = lin_init(x, c, &A);
+        const double rb = lin_room(x, c, &B);
+        const double rad = ra >= BIG ? BIGD : (double)ra;
+        const bool same = ra >= 2 ? rad == rb && (A.frozen ? B.frozen : (A.X == B.X && A.R == B.R && A.u == B.u))
+                                  : rb < 2.0;
+        bad += same ? 0 : 1;
+    }
+    return bad;
+}
+
+// advance(x, c, k) against k literal additions fl(x + c), on n pseudo-random
+// walks of up to 3000 steps, a third of them across zero.  Returns the number
+// of walks whose end point differs.
+extern "C" long advance_check(long n, uint64_t seed) {
+    using namespace pt::march;
+    uint64_t s = seed;
+    auto next = [&s]() {
+        s += 0x9E3779B97F4A7C15ull;
+        uint64_t z = s;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    auto unit = [&]() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0; };
+    long bad = 0;
+    for (long i = 0; i < n; i++) {
+        const int64_t k = 1 + (int64_t)(next() % 3000);
+        double c = unit() * ldexp(1.0, -(int)(next() % 20) - 4);
+        double x = unit() * ldexp(1.0, (int)(next() % 8) - 4);
+        if (i % 3 == 0) x = -c * (double)k * (0.2 + 0.6 * (unit() + 1.0) * 0.5);  // crosses zero within the walk
+        double lit = x;
+        for (int64_t j = 0; j < k; j++) lit = lit + c;
+        bad += advance(x, c, k) == lit ? 0 : 1;
+    }
+    return bad;
+}

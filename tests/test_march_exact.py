@@ -105,3 +105,19 @@ def test_march_respects_t_range(march_lib):
     rays = aimed_rays(rng, [278.0, 278.0, -800.0], [150, 160, 100], [280, 240, 200], 40)
     run_case(march_lib, sc, rays, 0.01, 4, min_t=0.001, max_t=900.0)
     run_case(march_lib, sc, rays, 0.01, 4, min_t=905.0, max_t=float("inf"))
+
+
+def test_lin_room_matches_lin_init(march_lib):
+    """The straight-line closed form the kernels use (lin_room) gives lin_init's
+    room and grid wherever lin_init applies, on 1M random (x, c) pairs with
+    binade edges, round-half-even ties, zero steps and negative x."""
+    march_lib.lin_room_check.argtypes = [C.c_long, C.c_uint64]
+    march_lib.lin_room_check.restype = C.c_long
+    assert march_lib.lin_room_check(1_000_000, 12345) == 0
+
+
+def test_advance_equals_literal_adds(march_lib):
+    """advance(x, c, k) is k literal f64 additions, across binades and zero."""
+    march_lib.advance_check.argtypes = [C.c_long, C.c_uint64]
+    march_lib.advance_check.restype = C.c_long
+    assert march_lib.advance_check(20_000, 777) == 0

@@ -141,7 +141,7 @@ int pt_renderer_num_devices(const pt_renderer *r);
  * the measured optimum): "engine" (0 auto, 1 megakernel,
  * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
  * "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
- * "wf_march_blocks_per_cu".  A new renderer takes them from the PT_*
+ * "wf_march_blocks_per_cu", "wf_side_priority".  A new renderer takes them from the PT_*
  * environment variables (PT_ENGINE=mega|wave, PT_WAVES, PT_WF_SLOTS, ...)
  * once; set_option changes them for every device of the renderer (not while
  * a render_start frame is in flight).  No knob changes the image: every

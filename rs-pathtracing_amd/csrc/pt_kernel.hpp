@@ -52,6 +52,7 @@ struct Tuning {
     int wf_march_slice = 256;        // PT_WF_MARCH_SLICE: march-queue run dealt to a block (0 = contiguous share)
     int wf_trace_slice = 256;        // PT_WF_TRACE_SLICE: live-list run dealt to a wf_trace block
     int wf_march_blocks_per_cu = 0;  // PT_WF_MARCH_BLOCKS_PER_CU: persistent march grid (0 = occupancy maximum)
+    int wf_side_priority = 0;        // PT_WF_SIDE_PRIORITY: the library's chunk streams' priority (-1 low, 0 normal, 1 high)
 };
 Tuning tuning_from_env();
 // 0 on success, PT_ERR_INVALID for an unknown name or a value out of range
@@ -75,6 +76,7 @@ struct WaveWorkspace {
     hipEvent_t done = nullptr;
     bool used = false;
     int device = -1;
+    int side_priority = 0;  // the priority the side streams were created with (Tuning::wf_side_priority)
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

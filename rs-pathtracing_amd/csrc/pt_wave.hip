@@ -948,7 +948,9 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (ws->device != dev) {  // streams and events belong to one device
+    if (ws->device != dev || ws->side_priority != ws->tune.wf_side_priority) {  // streams and events belong to one device
+        // the previous frame must be done with the streams and the workspace
+        if (ws->used && ws->done && (e = hipEventSynchronize(ws->done)) != hipSuccess) return e;
         for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
             if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
             if (ws->join[k]) (void)hipEventDestroy(ws->join[k]);
@@ -961,12 +963,18 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
         ws->fork = ws->reduced = ws->done = nullptr;
         ws->used = false;
         ws->device = dev;
+        ws->side_priority = ws->tune.wf_side_priority;
     }
     if (!ws->fork && (e = hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->done && (e = hipEventCreateWithFlags(&ws->done, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
     for (int k = 0; k < slots - 1; k++) {
-        if (!ws->side[k] && (e = hipStreamCreateWithFlags(&ws->side[k], hipStreamNonBlocking)) != hipSuccess) return e;
+        if (!ws->side[k]) {
+            int lo = 0, hi = 0;  // least and greatest priority (greatest is numerically lowest)
+            if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return e;
+            const int pr = ws->tune.wf_side_priority < 0 ? lo : (ws->tune.wf_side_priority > 0 ? hi : 0);
+            if ((e = hipStreamCreateWithPriority(&ws->side[k], hipStreamNonBlocking, pr)) != hipSuccess) return e;
+        }
         if (!ws->join[k] && (e = hipEventCreateWithFlags(&ws->join[k], hipEventDisableTiming)) != hipSuccess) return e;
     }
     return hipSuccess;

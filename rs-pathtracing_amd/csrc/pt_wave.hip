@@ -155,6 +155,9 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
     *y = ty * TILE + (((w >> 1) << 3) | (l >> 3));
 }
 
+#ifndef PT_WF_BPL
+#define PT_WF_BPL 1  // bounces a path may take per bounce launch while it needs no march
+#endif
 #ifndef PT_WF_LONG_R2
 #define PT_WF_LONG_R2 1.1  // closest approach^2 to the marched shape's centre (object space) of a predicted-long job
 #endif
@@ -190,6 +193,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         dev::Rng rng{0};
         uint32_t depth = 0;
         MemStack stk{v.ids, (size_t)v.cap, 0, nullptr};
+        // pending hit of the path (non-first iterations: from the state)
+        int who = -1;
+        double best = 0.0;
         if (live) {
             if (FIRST) {
                 id = i;
@@ -201,6 +207,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     rng.s = dev::sample_key(P.seed, (uint64_t)x + (uint64_t)y * P.width, v.s0 + sl);
                     ray = dev::camera_ray(P, x, y, rng);
                     depth = P.depth;
+                    stk.base = v.ids + id;  // (a second bounce in this launch pushes onto it)
+                    if (EXT) stk.vb = v.att + id;
                 }
             } else {
                 id = v.list[i];
@@ -209,38 +217,44 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
                 rng.s = v.rng[id];
                 const uint32_t meta = v.meta[id];
-                const int who0 = v.who[id];
-                const double t0 = v.t[id];
+                who = v.who[id];
+                best = v.t[id];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 if (EXT) stk.vb = v.att + id;
                 PT_BSTAMP(1)
+            }
+        }
+        // Up to PT_WF_BPL bounces of this path: shade the pending hit (the
+        // camera ray has none), trace the new ray; go on while the path lives
+        // and no marched shape's bound starts before its best hit.
+        bool need_march = false, long_job = false;
+        for (int b = 0; live; b++) {
+            if (!FIRST || b > 0) {
                 V3 leaf;
-                const bool ended = dev::shade<false, FK, EXT>(sc, who0, t0, ray, depth, stk, rng, P.s11, &leaf);
+                const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
                 PT_BSTAMP(2)
                 if (ended) {
                     // the leaf radiance and the stack depth; wf_reduce unwinds
                     // the attenuation stack (end_path)
                     end_path(v, id, stk, leaf);
                     live = false;
+                    PT_BSTAMP(3)
+                    break;
                 }
-                PT_BSTAMP(3)
             }
-        }
-        bool need_march = false, long_job = false;
-        if (live) {
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-            double best = __builtin_inf();
-            int who = -1;
+            best = __builtin_inf();
+            who = -1;
             dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
             PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
-            // march kernel repeats this select and marches)
+            // march kernel marches it)
             for (int k = 0; k < sc.nmarch && !need_march; k++) {
                 const int s = dev::uniform_load(&sc.march[k]);
-                const DBox b = dev::uniform_box(&sc.boxes[s]);
-                if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
+                const DBox bx = dev::uniform_box(&sc.boxes[s]);
+                if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
                 const DShape S = dev::uniform_shape(&sc.shapes[s]);
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
@@ -258,6 +272,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 }
             }
             PT_BSTAMP(5)
+            if (need_march || b + 1 >= PT_WF_BPL) break;
+        }
+        if (live) {
             v.ox[id] = ray.o.x;
             v.oy[id] = ray.o.y;
             v.oz[id] = ray.o.z;

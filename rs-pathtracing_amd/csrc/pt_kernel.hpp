@@ -53,6 +53,7 @@ struct Tuning {
     int wf_trace_slice = 256;        // PT_WF_TRACE_SLICE: live-list run dealt to a wf_trace block
     int wf_march_blocks_per_cu = 0;  // PT_WF_MARCH_BLOCKS_PER_CU: persistent march grid (0 = occupancy maximum)
     int wf_side_priority = 0;        // PT_WF_SIDE_PRIORITY: the library's chunk streams' priority (-1 low, 0 normal, 1 high)
+    int wf_pingpong = 0;             // PT_WF_PINGPONG: bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
 };
 Tuning tuning_from_env();
 // 0 on success, PT_ERR_INVALID for an unknown name or a value out of range
@@ -71,6 +72,7 @@ struct WaveWorkspace {
     static constexpr int MAX_SLOTS = 4;
     hipStream_t side[MAX_SLOTS - 1] = {};
     hipEvent_t fork = nullptr, join[MAX_SLOTS - 1] = {}, reduced = nullptr;
+    hipEvent_t bev = nullptr, mev = nullptr;  // the last bounce / march launch of the cross-stream chains (Tuning::wf_pingpong)
     // recorded on the launch stream after a frame's last use of the workspace;
     // the next frame (on any stream) waits for it
     hipEvent_t done = nullptr;

@@ -864,7 +864,9 @@ void wave_workspace_free(WaveWorkspace *ws) {
     if (ws->fork) (void)hipEventDestroy(ws->fork);
     if (ws->reduced) (void)hipEventDestroy(ws->reduced);
     if (ws->done) (void)hipEventDestroy(ws->done);
-    ws->fork = ws->reduced = ws->done = nullptr;
+    if (ws->bev) (void)hipEventDestroy(ws->bev);
+    if (ws->mev) (void)hipEventDestroy(ws->mev);
+    ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = nullptr;
     ws->used = false;
     timer_free(ws->timer);
     ws->timer = nullptr;
@@ -977,7 +979,9 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
         if (ws->fork) (void)hipEventDestroy(ws->fork);
         if (ws->reduced) (void)hipEventDestroy(ws->reduced);
         if (ws->done) (void)hipEventDestroy(ws->done);
-        ws->fork = ws->reduced = ws->done = nullptr;
+        if (ws->bev) (void)hipEventDestroy(ws->bev);
+        if (ws->mev) (void)hipEventDestroy(ws->mev);
+        ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = nullptr;
         ws->used = false;
         ws->device = dev;
         ws->side_priority = ws->tune.wf_side_priority;
@@ -985,6 +989,8 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     if (!ws->fork && (e = hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->done && (e = hipEventCreateWithFlags(&ws->done, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ws->bev && (e = hipEventCreateWithFlags(&ws->bev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ws->mev && (e = hipEventCreateWithFlags(&ws->mev, hipEventDisableTiming)) != hipSuccess) return e;
     for (int k = 0; k < slots - 1; k++) {
         if (!ws->side[k]) {
             int lo = 0, hi = 0;  // least and greatest priority (greatest is numerically lowest)
@@ -1112,40 +1118,63 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
     }
     const bool fused = tu.wf_fused && !ws->diag;
-    uint64_t c = 0;
+    // Chunks run in rounds of `slots`, chunk j of a round on stream j, and are
+    // enqueued iteration by iteration across the round.  With wf_pingpong the
+    // bounce launches form one chain across the streams (each waits for the
+    // previous one, in enqueue order), so one chunk's bounce (memory-bound)
+    // runs beside the other chunk's compaction and march (VALU-bound) instead
+    // of both chunks bouncing, then both marching, at the same time.
+    struct Chunk {
+        uint32_t g0, gt, s0;
+    };
+    std::vector<Chunk> chunk_list;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns, c++) {
-            const int k = (int)(c % (uint64_t)slots);
-            const hipStream_t cs = k == 0 ? st : ws->side[k - 1];
-            WfView &v = sl[k].v;
-            uint32_t *cp_blk = sl[k].cp_blk;
-            v.tile0 = P0.tile_begin + g0;
-            v.npix = gt * TILE * TILE;
-            v.s0 = s0;
-            v.ns = P0.spp - s0 < ns ? P0.spp - s0 : ns;
+        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns) chunk_list.push_back(Chunk{g0, gt, s0});
+    }
+    // wf_pingpong bit 0: chain the bounce launches; bit 1: chain the march launches
+    const bool pingpong = (tu.wf_pingpong & 1) && slots > 1, mchain = (tu.wf_pingpong & 2) && slots > 1;
+    bool chained = false, mchained = false;  // ws->bev / ws->mev hold a launch to wait for
+    for (size_t r0 = 0; r0 < chunk_list.size(); r0 += (size_t)slots) {
+        const int nr = (int)(chunk_list.size() - r0 < (size_t)slots ? chunk_list.size() - r0 : (size_t)slots);
+        for (int j = 0; j < nr; j++) {  // the round's chunks: views and cleared counters
+            const Chunk &ch = chunk_list[r0 + j];
+            const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
+            WfView &v = sl[j].v;
+            v.tile0 = P0.tile_begin + ch.g0;
+            v.npix = ch.gt * TILE * TILE;
+            v.s0 = ch.s0;
+            v.ns = P0.spp - ch.s0 < ns ? P0.spp - ch.s0 : ns;
             const uint32_t paths = v.ns * v.npix;
-            e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs);
-            if (e != hipSuccess) return e;
-            e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, cs);
-            if (e != hipSuccess) return e;
-            uint32_t bb = (paths + 255) / 256;
-            if (bb > PT_WF_BOUNCE_CAP) bb = PT_WF_BOUNCE_CAP;
-            // iteration 0: slots [0, paths) are the chunk's camera rays
-            if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-            if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);
-            else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
-            for (int it = 0; it < iters; it++) {
-                if (it > 0) {
-                    if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, cs)) != hipSuccess)
+                return e;
+        }
+        for (int it = 0; it < iters; it++) {
+            for (int j = 0; j < nr; j++) {
+                const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
+                WfView &v = sl[j].v;
+                uint32_t *cp_blk = sl[j].cp_blk;
+                const uint32_t paths = v.ns * v.npix;
+                uint32_t bb = (paths + 255) / 256;
+                if (bb > PT_WF_BOUNCE_CAP) bb = PT_WF_BOUNCE_CAP;
+                if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
+                // iteration 0: slots [0, paths) are the chunk's camera rays
+                if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
+                if (it == 0) {
+                    if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);
+                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves);
+                } else {
                     if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind, (uint32_t)tu.wf_trace_slice);
                     else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind, tu.wf_bounce_waves);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
-                    if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 }
-                if (it == iters - 1) break;  // the last bounce only shades
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                if (pingpong) {
+                    if ((e = hipEventRecord(ws->bev, cs)) != hipSuccess) return e;
+                    chained = true;
+                }
+                if (it == iters - 1) continue;  // the last bounce only shades
                 // live list for it + 1 and march queue for it, both id-sorted
                 if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
@@ -1155,6 +1184,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)
                     wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
@@ -1164,9 +1194,18 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                     wf_march<false, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                if (mchain) {
+                    if ((e = hipEventRecord(ws->mev, cs)) != hipSuccess) return e;
+                    mchained = true;
+                }
             }
-            // the per-pixel sums take the chunks in order
-            if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
+        }
+        // the per-pixel sums take the chunks in order
+        for (int j = 0; j < nr; j++) {
+            const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
+            WfView &v = sl[j].v;
+            const uint32_t s0 = v.s0;
+            if (slots > 1 && r0 + j > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
             if (sc.ext)
                 wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);

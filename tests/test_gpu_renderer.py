@@ -238,7 +238,7 @@ def test_tuning_options(pt, cornell):
     base = r.render(cam, ip, 3, seed=4)
     for name, value in [("wf_slots", 1), ("wf_slots", 4), ("wf_march_slice", 0), ("wf_bounce_waves", 2),
                         ("wf_march_blocks_per_cu", 1), ("wf_min_chunks", 3), ("engine", 1), ("mega_waves", 2),
-                        ("wf_side_priority", -1), ("wf_side_priority", 1)]:
+                        ("wf_side_priority", -1), ("wf_side_priority", 1), ("wf_pingpong", 1)]:
         r.set_option(name, value)
         assert r.get_option(name) == value
         assert np.array_equal(r.render(cam, ip, 3, seed=4), base), (name, value)

@@ -191,9 +191,8 @@ PT_HD double lin_room(double x, double c, Lin *L) {
 // edges: closed form inside each binade, literal adds in the thin zone at an
 // edge (and near zero).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
-PT_HD double advance(double x, double c, int64_t n_) {
+PT_HD double advance(double x, double c, double n) {
     PT_MHOOK(adv_begin);
-    double n = (double)n_;
     while (n > 0.0) {
         PT_MPROF(advance_loops);
         Lin L;
@@ -232,29 +231,25 @@ PT_HD void seg_step(double &x, double c, double &n) {
 // j <= (lim - t) / (|s| + delta) are in range; the quotient is shrunk by a
 // relative 1e-12 and one step for its own rounding.  Blocks only need a
 // lower bound: the last few steps before the range end are taken literally.
-PT_HD int64_t steps_in_range_lb(double t, double s, double start, double end, int64_t cap) {
-    const double lim = s > 0.0 ? end : start;
+PT_HD double steps_in_range_lb(double t, double s, double start, double end, double cap) {
     const double dist = s > 0.0 ? end - t : t - start;
-    if (!(dist >= 0.0)) return 0;
     const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
     // the quotient through a polished reciprocal (a few ulp): far inside the 1e-12 shrink
     const double k = floor(dist * approx_rcp(fabs(s) + delta) * (1.0 - 1e-12)) - 1.0;
-    (void)lim;
-    if (!(k >= 0.0)) return 1;
-    return k + 1.0 >= (double)cap ? cap : (int64_t)k + 1;
+    const double b = !(k >= 0.0) ? 1.0 : (k + 1.0 >= cap ? cap : k + 1.0);
+    return dist >= 0.0 ? b : 0.0;
 }
 
 // An upper bound on the index J of the first t_J outside [start, end] (the
 // step at which the reference's range check ends the pass with a miss):
 // t_j >= t + j (s - delta) (s > 0; mirrored for s < 0), so J <= floor(dist /
 // (|s| - delta)) + 1; grown by a relative 1e-12 and two steps for rounding.
-PT_HD int64_t steps_exit_ub(double t, double s, double start, double end) {
+PT_HD double steps_exit_ub(double t, double s, double start, double end) {
     const double dist = s > 0.0 ? end - t : t - start;
     const double delta = 1.1102230246251565e-16 * fmax(fabs(start), fabs(end));
     const double as = fabs(s);
-    if (!(dist >= 0.0) || !(as > 2.0 * delta)) return BIG;
     const double k = ceil(dist * approx_rcp(as - delta) * (1.0 + 1e-12)) + 2.0;  // reciprocal: see above
-    return k >= BIGD ? BIG : (int64_t)k;
+    return !(dist >= 0.0) || !(as > 2.0 * delta) || !(k < BIGD) ? BIGD : k;
 }
 
 // Largest b (<= cap) such that t_0 .. t_{b-1} of t_{j+1} = fl(t_j + s) all lie
@@ -453,9 +448,8 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 #define PT_EM_LEVELS 40  // halvings of a failed early-miss proof (the next proof restarts from a fresh guess)
 #endif
 template <int FK>
-PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn, int64_t target = 0,
-                          int max_levels = PT_MAX_LEVELS) {
-    const double Bd = (double)B;
+PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn, double target = 0.0,
+                         int max_levels = PT_MAX_LEVELS) {
     const double margin = poly_margin<FK>(F, P, Bd);
     double a[7];
     double bk = 1.0;
@@ -464,7 +458,7 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
         a[k] = sgn * P.g[k] * bk;
         bk *= Bd;
     }
-    if (a[0] <= margin) return 0;
+    if (a[0] <= margin) return 0.0;
     double c[7];
     c[0] = a[0];
     c[1] = a[0] + a[1] * (1.0 / 6.0);
@@ -473,7 +467,7 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
     c[4] = a[0] + a[1] * (2.0 / 3.0) + a[2] * 0.4 + a[3] * 0.2 + a[4] * (1.0 / 15.0);
     c[5] = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
     c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
-    if (PT_TARGET_SPLIT && target >= 2 && target < B) {
+    if (PT_TARGET_SPLIT && target >= 2.0 && target < Bd) {
         // One split at the step just before the predicted crossing: de
         // Casteljau at lambda >= target / B gives the control points of
         // [0, lambda B], a superset of the steps [1, target]; if they clear
@@ -481,7 +475,7 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
         // not needed.  lambda is target / B rounded up (an exact fma test),
         // and the lerps' rounding (6 levels, weights in [0, 1]) stays inside
         // the margin's 256 eps M part like the halvings' do.
-        const double td = (double)target;
+        const double td = target;
         double lam = td * approx_rcp(Bd);
         if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
         if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
@@ -530,8 +524,8 @@ PT_HD int64_t poly_prefix(const FParams &F, const Poly &P, int64_t B, double sgn
         }
     }
     PT_MHOOK(lv_end);
-    double b = floor(proven * Bd);
-    return b < 0.0 ? 0 : (int64_t)b;
+    const double b = floor(proven * Bd);
+    return b < 0.0 ? 0.0 : b;
 }
 
 // Predicted first crossing (in steps) of sgn*g: the quadratic part's first
@@ -623,7 +617,7 @@ struct MarchStats {
 struct MarchState {
     FParams F;  // which implicit function, and its constants
     double t, px, py, pz, r, s, start, end, dx, dy, dz;
-    int64_t lim;  // steps_in_range from the current point for this pass (-1: not known yet)
+    double lim;  // a lower bound on the steps in range from the current point for this pass (-1: not known yet)
     int pass, passes;
     uint32_t iters;  // guard: a march that has not ended after MARCH_GUARD iterations is dropped
     int adv;         // 1 while a proven block's exact advance is still walking binade segments
@@ -658,7 +652,7 @@ PT_HD void march_start(const FParams &F, double step0, int passes, double ox, do
     m->dz = dz;
     m->pass = 0;
     m->passes = passes;
-    m->lim = -1;
+    m->lim = -1.0;
     m->iters = 0;
     m->adv = 0;
     m->lit = 0;
@@ -719,9 +713,9 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
     // ---- try to jump a block of b steps (exact advance + sign proof)
     if (m.r != 0.0) {
         // the range limit moves with the sequence: computed once per pass
-        if (m.lim < 0) m.lim = steps_in_range_lb(m.t, s, m.start, m.end, (int64_t)1 << 24);
-        const int64_t bmax = m.lim;
-        if (bmax >= 2) {
+        if (m.lim < 0.0) m.lim = steps_in_range_lb(m.t, s, m.start, m.end, 16777216.0);
+        const double bmax = m.lim;
+        if (bmax >= 2.0) {
             Poly P;
             func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
             if (STATS) st->tries++;
@@ -729,7 +723,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             // crossing (the margin scales with the block, so a block far
             // longer than the crossing distance would drown the near part)
             const double sgn = m.r > 0.0 ? 1.0 : -1.0;
-            const double guess = poly_root_guess(P, sgn, (double)bmax);
+            const double guess = poly_root_guess(P, sgn, bmax);
             if (guess < PT_MIN_GUESS) {
                 PT_MTRACE(guess, 0, 0, bmax);
                 // the crossing is the next step or two: up to PT_FOLD_MAX
@@ -740,23 +734,24 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             // No crossing predicted before the range end: try to prove every
             // step up to (an upper bound on) the one that leaves the range;
             // then nothing can stop this pass first and the march misses.
-            const int64_t ub = PT_EARLY_MISS && guess >= (double)bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIG;
-            int64_t B = ub < BIG ? ub : (int64_t)(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
-            if (ub == BIG) B = B > bmax ? bmax : (B < 2 ? 2 : B);
+            const double ub = PT_EARLY_MISS && guess >= bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIGD;
+            const bool em = ub < BIGD;  // an early-miss proof
+            double B = em ? ub : floor(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
+            if (!em) B = B > bmax ? bmax : (B < 2.0 ? 2.0 : B);
             // the step just before the predicted crossing
-            const int64_t target = ub == BIG ? (int64_t)ceil(guess) - 1 : 0;
-            int64_t good = poly_prefix<FK>(m.F, P, B, sgn, target, ub == BIG ? PT_MAX_LEVELS : PT_EM_LEVELS);
+            const double target = em ? 0.0 : ceil(guess) - 1.0;
+            double good = poly_prefix<FK>(m.F, P, B, sgn, target, em ? PT_EM_LEVELS : PT_MAX_LEVELS);
             PT_MTRACE(guess, B, good, bmax);
-            if (ub < BIG && good >= ub) return M_MISS;
+            if (em && good >= ub) return M_MISS;
             good = good > bmax ? bmax : good;
-            if (good >= 2) {
+            if (good >= 2.0) {
                 // the block's exact advance runs one binade segment per
                 // coordinate per iteration (march_advance), so a lane whose
                 // coordinates cross many binades does not stall its wave
-                m.na[0] = m.na[1] = m.na[2] = m.na[3] = (double)good;
+                m.na[0] = m.na[1] = m.na[2] = m.na[3] = good;
                 m.lim -= good;
                 m.adv = 1;
-                if (PT_LIT_MAX > 0.0 && good < B) m.lit = (int)fmin(PT_LIT_MAX, fmax(1.0, ceil(guess - (double)good)));
+                if (PT_LIT_MAX > 0.0 && good < B) m.lit = (int)fmin(PT_LIT_MAX, fmax(1.0, ceil(guess - good)));
                 if (STATS) st->blocks++;
                 if (INLINE_ADV) {
                     // one loop per coordinate: a lane pays only for the binade
@@ -772,7 +767,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     // crossing: take that literal step in this iteration
                     if (PT_FOLD_LIT && good < B && m.lim >= 1) {
                         // more than one when the predicted crossing is past the first
-                        nlit = guess > (double)good + 1.0 ? PT_FOLD_MAX : 1;
+                        nlit = guess > good + 1.0 ? PT_FOLD_MAX : 1;
                         goto literal;
                     }
                 }
@@ -785,7 +780,7 @@ literal:
     // crossing ends the pass; the range check before each step after the
     // first is covered by lim >= 1
     for (;;) {
-        if (m.lim > 0) m.lim--;
+        if (m.lim > 0.0) m.lim -= 1.0;
         m.t += s;
         m.px += cx;
         m.py += cy;
@@ -799,13 +794,13 @@ literal:
         if ((m.r < 0.0 && next > 0.0) || (m.r > 0.0 && next < 0.0)) {
             m.s = s * -0.01;
             m.r = next;
-            m.lim = -1;
+            m.lim = -1.0;
             m.lit = 0;
             m.pass++;
             return m.pass >= m.passes ? M_DONE : M_RUNNING;
         }
         m.r = next;
-        if (PT_FOLD_MAX <= 1 || --nlit <= 0 || m.lim < 1) return M_RUNNING;
+        if (PT_FOLD_MAX <= 1 || --nlit <= 0 || m.lim < 1.0) return M_RUNNING;
     }
 }
 
@@ -828,8 +823,8 @@ PT_HD int march_phase(MarchState &m) {
     if (m.pass >= m.passes || m.iters + 1 > MARCH_GUARD) return MP_CHEAP;
     if (m.adv) return MP_ADV;
     if (m.t > m.end || m.t < m.start || m.lit > 0 || m.r == 0.0) return MP_CHEAP;
-    if (m.lim < 0) m.lim = steps_in_range_lb(m.t, m.s, m.start, m.end, (int64_t)1 << 24);
-    return m.lim >= 2 ? MP_PROOF : MP_CHEAP;
+    if (m.lim < 0.0) m.lim = steps_in_range_lb(m.t, m.s, m.start, m.end, 16777216.0);
+    return m.lim >= 2.0 ? MP_PROOF : MP_CHEAP;
 }
 
 // RayMarchingShape::ray_intersect for the Heart in object space (o, d):

@@ -26,6 +26,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "pt_funcs.hpp"
 
@@ -90,6 +91,17 @@ PT_HD double approx_rcp(double x) {
 #else
     return 1.0 / x;
 #endif
+}
+
+PT_HD uint64_t f64_to_bits(double x) {
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+PT_HD double bits_to_f64(uint64_t u) {
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
 }
 
 // floor(n / d) for integers 0 <= n, 1 <= d, n / d < 2^41, all exact in f64.
@@ -476,9 +488,9 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
         // and the lerps' rounding (6 levels, weights in [0, 1]) stays inside
         // the margin's 256 eps M part like the halvings' do.
         const double td = target;
-        double lam = td * approx_rcp(Bd);
-        if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
-        if (fma(lam, Bd, -td) < 0.0) lam = nextafter(lam, 2.0);
+        double lam = td * approx_rcp(Bd);  // > 0: the next double up is one more in its bits
+        if (fma(lam, Bd, -td) < 0.0) lam = bits_to_f64(f64_to_bits(lam) + 1);
+        if (fma(lam, Bd, -td) < 0.0) lam = bits_to_f64(f64_to_bits(lam) + 1);
         if (fma(lam, Bd, -td) >= 0.0 && lam <= 1.0) {
             double w[7];
 #pragma unroll
@@ -545,24 +557,17 @@ PT_HD double poly_eval(const Poly &P, double j, double *dg) {
 // A heuristic only (it sizes the block; the proof decides what is skipped), so
 // it divides through the hardware reciprocal.
 PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
-    double L = sgn * P.g[0], S = sgn * P.g[1], Q = sgn * P.g[2];
-    if (L <= 0.0) return 1.0;
-    double r;
-    if (Q == 0.0) {
-        r = S < 0.0 ? L * approx_rcp(-S) : cap;
-    } else {
-        double disc = S * S - 4.0 * Q * L;
-        if (disc < 0.0) {
-            r = cap;  // no real root of the quadratic
-        } else {
-            double sq = sqrt(disc);
-            const double i2q = approx_rcp(2.0 * Q);
-            double r1 = (-S - sq) * i2q, r2 = (-S + sq) * i2q;
-            double lo = fmin(r1, r2), hi = fmax(r1, r2);
-            r = lo > 0.0 ? lo : (hi > 0.0 ? hi : cap);
-        }
-    }
-    r = fmin(cap, r);
+    // straight-line: every case computed, then selected (the values are the
+    // branchy form's wherever it used them)
+    const double L = sgn * P.g[0], S = sgn * P.g[1], Q = sgn * P.g[2];
+    const double disc = S * S - 4.0 * Q * L;
+    const double sq = sqrt(fmax(disc, 0.0));
+    const double i2q = approx_rcp(2.0 * Q);
+    const double r1 = (-S - sq) * i2q, r2 = (-S + sq) * i2q;
+    const double lo = fmin(r1, r2), hi = fmax(r1, r2);
+    const double rq = disc < 0.0 ? cap : (lo > 0.0 ? lo : (hi > 0.0 ? hi : cap));  // (no real root: no crossing)
+    const double rl = S < 0.0 ? L * approx_rcp(-S) : cap;
+    double r = fmin(cap, Q == 0.0 ? rl : rq);
 #pragma unroll
     for (int it = 0; it < PT_NEWTON; it++) {
         double d, g = poly_eval(P, r, &d);
@@ -571,7 +576,7 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
         if (!(nr > 0.0)) break;
         r = fmin(cap, nr);
     }
-    return r;
+    return L <= 0.0 ? 1.0 : r;
 }
 
 // ------------------------------------------------------- the march

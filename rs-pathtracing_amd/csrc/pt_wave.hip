@@ -24,10 +24,14 @@
 //                  order to the running sum (the reference's in-order sum),
 //                  and divides by spp after the last chunk.
 //
-// Path state lives in HBM, structure-of-arrays, one slot per (pixel, sample)
-// of a chunk: ~140 B per path for depth <= 8.  Queue pushes are wave-
-// aggregated (one atomic per wave), which keeps 8x8 pixel blocks together in
-// the lists.  Every value is computed by the same device functions, in the
+// Path state lives in HBM, structure-of-arrays, dense by position: bounce
+// `it` reads its k-th input from one state set at the position the live list
+// names and writes it at position k of the other set (76 B per path), so the
+// later kernels read a dense, id-ordered subsequence of the previous bounce's
+// outputs (not a sparse one of the chunk's slots).  What a path leaves for
+// the per-pixel reduce (leaf radiance, attenuation ids) is kept per slot
+// (pixel, sample).  Order-preserving compaction keeps 8x8 pixel blocks
+// together in the lists.  Every value is computed by the same device functions, in the
 // same per-path order, as the megakernel and the oracle: the frame is
 // bit-identical.
 #include <hip/hip_runtime.h>
@@ -43,19 +47,31 @@ namespace pt {
 using dev::Ray;
 using dev::V3;
 
-// Device view of the workspace for one chunk.
-struct WfView {
+// Path state between kernels, structure of arrays, dense by position: the
+// bounce kernel of iteration `it` reads path k of its input list at position
+// list[k] of one set and writes it at position k of the other (the two sets
+// alternate by iteration), so every later kernel reads a dense, id-ordered
+// subsequence of the previous bounce's outputs instead of a sparse one of the
+// chunk's slots.  The slot id (sample, pixel) travels with the path.
+struct PathSoA {
     double *ox, *oy, *oz, *dx, *dy, *dz, *t;  // ray, best hit t
     uint64_t *rng;
     int32_t *who;    // best hit shape (-1: miss)
     uint32_t *meta;  // depth | stack count << 8
+    uint32_t *sid;   // slot id of the path
+};
+
+// Device view of the workspace for one chunk.
+struct WfView {
+    PathSoA in, out;  // the bounce reads `in` (by list position) and writes `out` (by its input index)
+    uint32_t *fin;   // per slot: attenuation-stack depth when the path ended (wf_reduce unwinds it)
     uint32_t *ids;   // attenuation-id stack: entry k of a path at ids[k * cap + id]
     double *att;     // textured attenuation values (EXT builds): (k * 3 + c) * cap + id
     double *rx, *ry, *rz;  // sample radiance of finished paths
-    uint8_t *status;  // per slot after a bounce: bit 0 path alive, bit 1 needs a march
-    uint32_t *list, *mq;  // id-sorted live list and march queue of the current iteration
+    uint8_t *status;  // per output position of a bounce: bit 0 path alive, bit 1 needs a march, bit 2 long march
+    uint32_t *list, *mq;  // positions (in `out` of the previous / current bounce) of the live paths and march jobs
     // march jobs pre-selected by the bounce kernel (scenes with one ray-marched
-    // shape, PT_WF_PRESELECT): object-space ray and bound interval per slot,
+    // shape, PT_WF_PRESELECT): object-space ray and bound interval per position,
     // 64 B each (o, d, start, end); null when the march kernel selects itself
     double2 *jo;
     uint32_t *cnt;  // per iteration: [0] live-list count, [1] march-queue count, [2..3] unused
@@ -136,7 +152,23 @@ __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const Mem
     v.rx[id] = leaf.x;
     v.ry[id] = leaf.y;
     v.rz[id] = leaf.z;
-    v.meta[id] = (uint32_t)stk.n << 8;
+    v.fin[id] = (uint32_t)stk.n;
+}
+
+// A live path's state at output position k.
+__device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
+                                           int who, uint64_t rng, uint32_t meta) {
+    S.ox[k] = ray.o.x;
+    S.oy[k] = ray.o.y;
+    S.oz[k] = ray.o.z;
+    S.dx[k] = ray.d.x;
+    S.dy[k] = ray.d.y;
+    S.dz[k] = ray.d.z;
+    S.t[k] = best;
+    S.who[k] = who;
+    S.rng[k] = rng;
+    S.meta[k] = meta;
+    S.sid[k] = id;
 }
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
@@ -211,14 +243,16 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     if (EXT) stk.vb = v.att + id;
                 }
             } else {
-                id = v.list[i];
+                const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
-                ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
-                ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
-                rng.s = v.rng[id];
-                const uint32_t meta = v.meta[id];
-                who = v.who[id];
-                best = v.t[id];
+                const PathSoA &S = v.in;
+                id = S.sid[p];
+                ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
+                ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
+                rng.s = S.rng[p];
+                const uint32_t meta = S.meta[p];
+                who = S.who[p];
+                best = S.t[p];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
@@ -260,7 +294,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
                 if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
-                    double2 *j = v.jo + (size_t)id * 4;
+                    double2 *j = v.jo + (size_t)i * 4;
                     j[0] = make_double2(o.x, o.y);
                     j[1] = make_double2(o.z, d.x);
                     j[2] = make_double2(d.y, d.z);
@@ -284,19 +318,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             PT_BSTAMP(5)
             if (need_march || b + 1 >= PT_WF_BPL) break;
         }
-        if (live) {
-            v.ox[id] = ray.o.x;
-            v.oy[id] = ray.o.y;
-            v.oz[id] = ray.o.z;
-            v.dx[id] = ray.d.x;
-            v.dy[id] = ray.d.y;
-            v.dz[id] = ray.d.z;
-            v.t[id] = best;
-            v.who[id] = who;
-            v.rng[id] = rng.s;
-            v.meta[id] = depth | ((uint32_t)stk.n << 8);
-        }
-        if (i < count) v.status[id] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
+        if (live) store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+        if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
@@ -330,7 +353,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
     uint32_t q = threadIdx.x;
     bool have = q < per && pos(q) < count;
     bool fresh = true;
-    uint32_t id = 0, depth = 0;
+    uint32_t id = 0, k = 0, depth = 0;  // slot id, input (= output) position
     Ray ray;
     ray.o = ray.d = dev::v3(0.0, 0.0, 0.0);
     dev::Rng rng{0};
@@ -341,13 +364,14 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
         bool done = false, shade_now = true;
         if (fresh) {
             fresh = false;
+            k = pos(q);
             if (FIRST) {
                 shade_now = false;
-                id = pos(q);
+                id = k;
                 uint32_t x, y, sl, pl;
                 slot_pixel(P, v, id, &x, &y, &sl, &pl);
                 if (x >= P.width || y >= P.height || sl >= v.ns) {
-                    v.status[id] = 0;
+                    v.status[k] = 0;
                     done = true;
                 } else {
                     rng.s = dev::sample_key(P.seed, (uint64_t)x + (uint64_t)y * P.width, v.s0 + sl);
@@ -358,24 +382,26 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
                     if (EXT) stk.vb = v.att + id;
                 }
             } else {
-                id = v.list[pos(q)];
-                ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
-                ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
-                rng.s = v.rng[id];
-                const uint32_t meta = v.meta[id];
+                const uint32_t p = v.list[k];
+                const PathSoA &S = v.in;
+                id = S.sid[p];
+                ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
+                ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
+                rng.s = S.rng[p];
+                const uint32_t meta = S.meta[p];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 if (EXT) stk.vb = v.att + id;
-                who = v.who[id];
-                best = v.t[id];
+                who = S.who[p];
+                best = S.t[p];
             }
         }
         if (!done && shade_now) {
             V3 leaf;
             if (dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf)) {
                 end_path(v, id, stk, leaf);
-                v.status[id] = 0;
+                v.status[k] = 0;
                 done = true;
             }
         }
@@ -385,8 +411,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
             who = -1;
             dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
             bool need_march = false;
-            for (int k = 0; k < sc.nmarch && !need_march; k++) {
-                const int s = dev::uniform_load(&sc.march[k]);
+            for (int km = 0; km < sc.nmarch && !need_march; km++) {
+                const int s = dev::uniform_load(&sc.march[km]);
                 const DBox b = dev::uniform_box(&sc.boxes[s]);
                 if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
                 const DShape S = dev::uniform_shape(&sc.shapes[s]);
@@ -394,7 +420,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
                 if (need_march && v.jo) {
-                    double2 *j = v.jo + (size_t)id * 4;
+                    double2 *j = v.jo + (size_t)k * 4;
                     j[0] = make_double2(o.x, o.y);
                     j[1] = make_double2(o.z, d.x);
                     j[2] = make_double2(d.y, d.z);
@@ -402,17 +428,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
                 }
             }
             if (need_march) {
-                v.ox[id] = ray.o.x;
-                v.oy[id] = ray.o.y;
-                v.oz[id] = ray.o.z;
-                v.dx[id] = ray.d.x;
-                v.dy[id] = ray.d.y;
-                v.dz[id] = ray.d.z;
-                v.t[id] = best;
-                v.who[id] = who;
-                v.rng[id] = rng.s;
-                v.meta[id] = depth | ((uint32_t)stk.n << 8);
-                v.status[id] = 3;
+                store_path(v.out, k, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+                v.status[k] = 3;
                 done = true;
             }
         }
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
     }
 }
 
-// Order-preserving compaction of the status bytes into the two id lists
+// Order-preserving compaction of the status bytes into the two position lists
 // (live paths: bit 0, march jobs: bit 1) in three small launches: per-tile
 // counts (16 statuses per thread, one 16-byte load), one scan over the tile
 // counts, and an ordered scatter.  Neighbouring pixels stay in neighbouring
@@ -472,10 +489,31 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
     return before + inc - x;
 }
 
+// The thread's 16 statuses; positions at or past the bounce's input count n
+// (stale bytes of earlier iterations) read as 0.
+__device__ __forceinline__ uint4 cp_load(const uint8_t *__restrict__ st, const uint32_t *n_dev, uint32_t n_host) {
+    const uint32_t n = n_dev ? *n_dev : n_host;
+    const uint32_t b = blockIdx.x * CP_TILE + threadIdx.x * CP_ITEMS;
+    if (b >= n) return make_uint4(0u, 0u, 0u, 0u);
+    uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    if (n - b < (uint32_t)CP_ITEMS) {
+        const uint32_t k = n - b;  // bytes kept: 1 .. 15
+        uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t keep = k >= 4u * (j + 1) ? 4u : (k > 4u * j ? k - 4u * j : 0u);
+            w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+        }
+        q = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return q;
+}
+
 // per tile: (live, long march, short march) counts in blk[3 * tile ..]
-__global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk) {
+__global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk,
+                                                const uint32_t *__restrict__ n_dev, uint32_t n_host) {
     __shared__ uint32_t lds[12];
-    const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    const uint4 q = cp_load(st, n_dev, n_host);
     uint32_t l, m, g, tl, tg, ts;
     cp_bits(q, &l, &m, &g);
     block_exscan(l, &tl, lds);
@@ -519,10 +557,11 @@ __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint3
 
 __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st, const uint32_t *__restrict__ blk,
                                                   const uint32_t *__restrict__ n_long, uint32_t *__restrict__ live_out,
-                                                  uint32_t *__restrict__ march_out) {
+                                                  uint32_t *__restrict__ march_out, const uint32_t *__restrict__ n_dev,
+                                                  uint32_t n_host) {
     __shared__ uint32_t lds[12];
     const size_t base = (size_t)blockIdx.x * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
-    const uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    const uint4 q = cp_load(st, n_dev, n_host);
     uint32_t l, m, g, tl, tg, ts;
     cp_bits(q, &l, &m, &g);
     uint32_t ol = blk[3 * blockIdx.x] + block_exscan(l, &tl, lds);
@@ -575,12 +614,12 @@ struct MarchJob {
     int who;
 };
 
-__device__ __forceinline__ void load_job(const WfView &v, uint32_t id, MarchJob *j) {
-    j->id = id;
-    j->ray.o = dev::v3(v.ox[id], v.oy[id], v.oz[id]);
-    j->ray.d = dev::v3(v.dx[id], v.dy[id], v.dz[id]);
-    j->best = v.t[id];
-    j->who = v.who[id];
+__device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob *j) {
+    j->id = p;
+    j->ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
+    j->ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
+    j->best = S.t[p];
+    j->who = S.who[p];
 }
 
 // DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
@@ -639,18 +678,18 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
 #ifdef PT_TIMING_CONVERGED  // timing experiment only: every lane of an aligned run of 64 takes the run's first job
         k = (k / 64) * 64;
 #endif
-        const uint32_t id = mq[k];
+        const uint32_t id = mq[k];  // position in the bounce's output
         if (pre) {
             cur.id = id;
-            cur.best = v.t[id];
-            cur.who = v.who[id];
+            cur.best = v.out.t[id];
+            cur.who = v.out.who[id];
             const double2 *j = v.jo + (size_t)id * 4;
             const double2 a = j[0], b = j[1], c = j[2], e = j[3];
             march::march_start<FK>(F0, step0, passes0, a.x, a.y, b.x, b.y, c.x, c.y, e.x, e.y, &ms);
             marching = true;
             mshape = s0;
         } else {
-            load_job(v, id, &cur);
+            load_job(v.out, id, &cur);
         }
     };
     if (have) start_job(pos(q));
@@ -743,15 +782,15 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 const double fbest = cur.best;
                 const int fwho = cur.who;
                 if (!PT_WF_STORE_LATE) {
-                    v.t[fid] = fbest;
-                    v.who[fid] = fwho;
+                    v.out.t[fid] = fbest;
+                    v.out.who[fid] = fwho;
                 }
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
                 if (have) start_job(pos(q));
                 if (PT_WF_STORE_LATE) {
-                    v.t[fid] = fbest;
-                    v.who[fid] = fwho;
+                    v.out.t[fid] = fbest;
+                    v.out.who[fid] = fwho;
                 }
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
@@ -799,7 +838,7 @@ __global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, W
     V3 a = first ? dev::v3(0.0, 0.0, 0.0) : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
     for (uint32_t s = 0; s < v.ns; s++) {
         const size_t id = (size_t)s * v.npix + pl;
-        MemStack stk{v.ids + id, (size_t)v.cap, (int)(v.meta[id] >> 8), EXT ? v.att + id : nullptr};
+        MemStack stk{v.ids + id, (size_t)v.cap, (int)v.fin[id], EXT ? v.att + id : nullptr};
         a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(v.rx[id], v.ry[id], v.rz[id])));
     }
     if (last) {
@@ -1022,6 +1061,7 @@ constexpr uint32_t MIN_CHUNK_PATHS = 1u << 21;
 struct Slot {
     WfView v;
     uint32_t *cp_blk;
+    PathSoA set[2];  // iteration it reads set[it & 1] and writes set[(it + 1) & 1]
 };
 
 template <int NW>
@@ -1068,7 +1108,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
     // pre-selected march jobs: one marched shape, PT_WF_PRESELECT
     const bool presel = PT_WF_PRESELECT && sc.nmarch == 1 && !ws->diag;
-    const size_t slot_bytes = al((size_t)cap * 8) * 11 + (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 4 +
+    // two path-state sets (8 + 3 words per path each), sample radiances, lists, end depths
+    const size_t slot_bytes = al((size_t)cap * 8) * 19 + (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 9 +
                               al((size_t)cap * 4 * (P0.depth + 1)) +
                               al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 12) + al(cnt_words * 4) +
                               al(att_bytes);
@@ -1085,16 +1126,21 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     Slot sl[WaveWorkspace::MAX_SLOTS];
     for (int k = 0; k < slots; k++) {
         WfView &v = sl[k].v;
-        v.ox = (double *)take((size_t)cap * 8);
-        v.oy = (double *)take((size_t)cap * 8);
-        v.oz = (double *)take((size_t)cap * 8);
-        v.dx = (double *)take((size_t)cap * 8);
-        v.dy = (double *)take((size_t)cap * 8);
-        v.dz = (double *)take((size_t)cap * 8);
-        v.t = (double *)take((size_t)cap * 8);
-        v.rng = (uint64_t *)take((size_t)cap * 8);
-        v.who = (int32_t *)take((size_t)cap * 4);
-        v.meta = (uint32_t *)take((size_t)cap * 4);
+        for (int h = 0; h < 2; h++) {
+            PathSoA &S = sl[k].set[h];
+            S.ox = (double *)take((size_t)cap * 8);
+            S.oy = (double *)take((size_t)cap * 8);
+            S.oz = (double *)take((size_t)cap * 8);
+            S.dx = (double *)take((size_t)cap * 8);
+            S.dy = (double *)take((size_t)cap * 8);
+            S.dz = (double *)take((size_t)cap * 8);
+            S.t = (double *)take((size_t)cap * 8);
+            S.rng = (uint64_t *)take((size_t)cap * 8);
+            S.who = (int32_t *)take((size_t)cap * 4);
+            S.meta = (uint32_t *)take((size_t)cap * 4);
+            S.sid = (uint32_t *)take((size_t)cap * 4);
+        }
+        v.fin = (uint32_t *)take((size_t)cap * 4);
         v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
         v.rx = (double *)take((size_t)cap * 8);
         v.ry = (double *)take((size_t)cap * 8);
@@ -1159,9 +1205,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             v.s0 = ch.s0;
             v.ns = P0.spp - ch.s0 < ns ? P0.spp - ch.s0 : ns;
             const uint32_t paths = v.ns * v.npix;
+            (void)paths;  // (every bounce writes the status of each of its inputs; compaction reads no further)
             if ((e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(v.status, 0, (size_t)((paths + CP_TILE - 1) / CP_TILE) * CP_TILE, cs)) != hipSuccess)
-                return e;
         }
         for (int it = 0; it < iters; it++) {
             for (int j = 0; j < nr; j++) {
@@ -1169,6 +1214,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 WfView &v = sl[j].v;
                 uint32_t *cp_blk = sl[j].cp_blk;
                 const uint32_t paths = v.ns * v.npix;
+                v.in = sl[j].set[it & 1];
+                v.out = sl[j].set[(it + 1) & 1];
                 uint32_t bb = (paths + 255) / 256;
                 if (bb > PT_WF_BOUNCE_CAP) bb = PT_WF_BOUNCE_CAP;
                 if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
@@ -1191,10 +1238,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 // live list for it + 1 and march queue for it, both id-sorted
                 if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
-                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk);
+                const uint32_t *n_in = it == 0 ? nullptr : &v.cnt[it * 4 + 0];  // the bounce's input count
+                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, n_in, paths);
                 cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
                                                 &v.cnt[it * 4 + 2]);
-                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq);
+                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq, n_in, paths);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;

@@ -47,6 +47,9 @@
 #ifndef PT_MTRACE
 #define PT_MTRACE(guess, B, good, bmax) ((void)0)
 #endif
+#ifndef PT_MREG  // device region timing (variant builds with PT_MARCH_REGIONS, pt_wave.hip)
+#define PT_MREG(what) ((void)0)
+#endif
 #ifndef PT_MCAPTURE
 #define PT_MCAPTURE(step0, passes, ox, oy, oz, dx, dy, dz) ((void)0)
 #endif
@@ -201,11 +204,32 @@ PT_HD double lin_room(double x, double c, Lin *L) {
 
 // x after n literal additions fl(x + c), exactly, across any number of binade
 // edges: closed form inside each binade, literal adds in the thin zone at an
-// edge (and near zero).  Each coordinate's sequence is independent of the
+// edge and within PT_ADV_NZ |c| of zero (a coordinate crossing zero passes
+// ~2 log2(|x| / |c|) binades; the ones near zero hold a few steps each, and a
+// closed-form segment costs ~150 instructions against ~5 per literal add: C2
+// one-stream march 183 -> 172 ms).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
+#ifndef PT_ADV_NZB
+#define PT_ADV_NZB 4  // literal adds per trip in the near-zero zone
+#endif
+#ifndef PT_ADV_NZ
+#define PT_ADV_NZ 24.0  // |x| below this many |c|: literal adds (the binades there hold a few steps each; 0: off)
+#endif
 PT_HD double advance(double x, double c, double n) {
     PT_MHOOK(adv_begin);
     while (n > 0.0) {
+        if (PT_ADV_NZ > 0.0 && fabs(x) < PT_ADV_NZ * fabs(c)) {
+            // near zero every binade holds only a few steps: PT_ADV_NZB
+            // literal adds per trip instead of one closed-form segment per binade
+#pragma unroll
+            for (int j = 0; j < PT_ADV_NZB; j++) {
+                PT_MPROF(lit_adds);
+                const bool go = n > 0.0;
+                x = go ? x + c : x;
+                n = go ? n - 1.0 : n;
+            }
+            continue;
+        }
         PT_MPROF(advance_loops);
         Lin L;
         const double room = lin_room(x, c, &L);
@@ -226,6 +250,11 @@ PT_HD double advance(double x, double c, double n) {
 // One segment of advance(): the closed form to the end of x's binade segment
 // (and the literal add leaving it), or one literal add in an edge zone.
 PT_HD void seg_step(double &x, double c, double &n) {
+    if (PT_ADV_NZ > 0.0 && fabs(x) < PT_ADV_NZ * fabs(c)) {  // near zero: a literal add (see advance)
+        x = x + c;
+        n -= 1.0;
+        return;
+    }
     Lin L;
     const double room = lin_room(x, c, &L);
     const double k = room >= 2.0 ? (room < n ? room : n) : 0.0;
@@ -507,6 +536,7 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
     }
     double lo = 0.0, len = 1.0, proven = 0.0;  // in units of B
     PT_MHOOK(lv_begin);
+    PT_MREG(halve_begin);
     for (int level = 0; level < max_levels; level++) {
         PT_MPROF(evals);
         double mn = fmin(fmin(fmin(c[1], c[2]), fmin(c[3], c[4])), fmin(fmin(c[5], c[6]), c[0]));
@@ -535,6 +565,7 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
             for (int i = 0; i < 7; i++) c[i] = l[i];
         }
     }
+    PT_MREG(halve_end);
     PT_MHOOK(lv_end);
     const double b = floor(proven * Bd);
     return b < 0.0 ? 0.0 : b;
@@ -722,6 +753,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
         const double bmax = m.lim;
         if (bmax >= 2.0) {
             Poly P;
+            PT_MREG(poly_begin);
             func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
             if (STATS) st->tries++;
             // longest provable prefix of a block sized from the predicted
@@ -729,6 +761,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             // longer than the crossing distance would drown the near part)
             const double sgn = m.r > 0.0 ? 1.0 : -1.0;
             const double guess = poly_root_guess(P, sgn, bmax);
+            PT_MREG(poly_end);
             if (guess < PT_MIN_GUESS) {
                 PT_MTRACE(guess, 0, 0, bmax);
                 // the crossing is the next step or two: up to PT_FOLD_MAX
@@ -745,7 +778,9 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             if (!em) B = B > bmax ? bmax : (B < 2.0 ? 2.0 : B);
             // the step just before the predicted crossing
             const double target = em ? 0.0 : ceil(guess) - 1.0;
+            PT_MREG(prefix_begin);
             double good = poly_prefix<FK>(m.F, P, B, sgn, target, em ? PT_EM_LEVELS : PT_MAX_LEVELS);
+            PT_MREG(prefix_end);
             PT_MTRACE(guess, B, good, bmax);
             if (em && good >= ub) return M_MISS;
             good = good > bmax ? bmax : good;
@@ -761,6 +796,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                 if (INLINE_ADV) {
                     // one loop per coordinate: a lane pays only for the binade
                     // segments each coordinate actually crosses
+                    PT_MREG(adv_begin);
                     m.t = advance(m.t, s, good);
                     m.px = advance(m.px, cx, good);
                     m.py = advance(m.py, cy, good);
@@ -768,6 +804,7 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
                     m.adv = 0;
                     m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
+                    PT_MREG(adv_end);
                     // a prefix that stopped short of B ends just before the
                     // crossing: take that literal step in this iteration
                     if (PT_FOLD_LIT && good < B && m.lim >= 1) {
@@ -784,6 +821,7 @@ literal:
     // ---- literal steps (ray_marching.rs:37-51): nlit of them while no
     // crossing ends the pass; the range check before each step after the
     // first is covered by lim >= 1
+    PT_MREG(lit_begin);
     for (;;) {
         if (m.lim > 0.0) m.lim -= 1.0;
         m.t += s;

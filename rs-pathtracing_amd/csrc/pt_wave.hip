@@ -39,6 +39,45 @@
 #include <cstdlib>
 #include <vector>
 
+#ifdef PT_MARCH_REGIONS
+// Tuning builds only: wave wall-clock (s_memtime) spent in each region of
+// the march kernel (pt_march.hpp's PT_MREG points), as seen by the wave's
+// first active lane, summed over all waves (pt_march_regions).
+namespace pt {
+namespace mreg {
+enum { R_ITER, R_POLY, R_PREFIX, R_HALVE, R_ADV, R_LIT, R_REFILL, R_TOTAL, R_N };
+__device__ unsigned long long g_acc[R_N];
+__shared__ unsigned long long t0[4][R_N], acc[4][R_N];
+__device__ __forceinline__ unsigned long long now() {
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__device__ __forceinline__ bool leader() {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    return lane == (uint32_t)__builtin_ctzll(__ballot(1));
+}
+__device__ __forceinline__ void begin(int r) {
+    if (leader()) t0[threadIdx.x >> 6][r] = now();
+}
+__device__ __forceinline__ void end(int r) {
+    if (leader()) acc[threadIdx.x >> 6][r] += now() - t0[threadIdx.x >> 6][r];
+}
+__device__ __forceinline__ void poly_begin() { begin(R_POLY); }
+__device__ __forceinline__ void poly_end() { end(R_POLY); }
+__device__ __forceinline__ void prefix_begin() { begin(R_PREFIX); }
+__device__ __forceinline__ void prefix_end() { end(R_PREFIX); }
+__device__ __forceinline__ void halve_begin() { begin(R_HALVE); }
+__device__ __forceinline__ void halve_end() { end(R_HALVE); }
+__device__ __forceinline__ void adv_begin() { begin(R_ADV); }
+__device__ __forceinline__ void adv_end() { end(R_ADV); }
+__device__ __forceinline__ void lit_begin() { begin(R_LIT); }
+}  // namespace mreg
+}  // namespace pt
+#define PT_MREG(what) pt::mreg::what()
+#endif
+
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
 
@@ -692,6 +731,11 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             load_job(v.out, id, &cur);
         }
     };
+#ifdef PT_MARCH_REGIONS
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < mreg::R_N; k++) mreg::t0[threadIdx.x >> 6][k] = mreg::acc[threadIdx.x >> 6][k] = 0;
+    const unsigned long long t_kernel = mreg::now();
+#endif
     if (have) start_job(pos(q));
     V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
@@ -745,7 +789,17 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
             bool done = false;
             if (marching) {
+#ifdef PT_MARCH_REGIONS
+                mreg::begin(mreg::R_ITER);
                 const int st = march::march_step<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
+                mreg::end(mreg::R_ITER);
+                if (mreg::leader() && mreg::t0[threadIdx.x >> 6][mreg::R_LIT]) {  // a literal loop ran: close it
+                    mreg::acc[threadIdx.x >> 6][mreg::R_LIT] += mreg::now() - mreg::t0[threadIdx.x >> 6][mreg::R_LIT];
+                    mreg::t0[threadIdx.x >> 6][mreg::R_LIT] = 0;
+                }
+#else
+                const int st = march::march_step<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
+#endif
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -775,6 +829,9 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 done = !marching;
             }
             if (done) {
+#ifdef PT_MARCH_REGIONS
+                mreg::begin(mreg::R_REFILL);
+#endif
                 // vmcnt counts loads and stores in issue order: a store issued
                 // before the next job's loads makes the wait for those loads a
                 // wait for the store's completion too
@@ -796,9 +853,18 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
                 }
+#ifdef PT_MARCH_REGIONS
+                mreg::end(mreg::R_REFILL);
+#endif
             }
         }
     }
+#ifdef PT_MARCH_REGIONS
+    if ((threadIdx.x & 63) == 0) {
+        mreg::acc[threadIdx.x >> 6][mreg::R_TOTAL] = mreg::now() - t_kernel;
+        for (int k = 0; k < mreg::R_N; k++) atomicAdd(&mreg::g_acc[k], mreg::acc[threadIdx.x >> 6][k]);
+    }
+#endif
     if (DIAG && (threadIdx.x & 63) == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         if (mask_prev >= 0) {
@@ -1286,6 +1352,18 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     ws->used = true;
     return hipSuccess;
 }
+
+#ifdef PT_MARCH_REGIONS
+// Region wave-cycles of the march kernel since the last clear (tuning builds).
+extern "C" int pt_march_regions(unsigned long long *out, int clear) {
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(mreg::g_acc), sizeof(mreg::g_acc)) != hipSuccess) return -1;
+    if (clear) {
+        static const unsigned long long z[mreg::R_N] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mreg::g_acc), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
                               WaveWorkspace *ws, int fkind) {

@@ -23,7 +23,7 @@ static bool g_capture = false;
 static long g_hist_adv[64], g_hist_blockmax[64], g_hist_levels[64];
 static int g_cur_adv = 0, g_block_max = 0, g_cur_levels = 0;
 struct Prof {
-    unsigned long long lin_init, advance_loops, sir_inside, evals, iters, lin_fail_zero, lin_fail_q, lin_fail_tie, lin_fail_zone;
+    unsigned long long lin_init, advance_loops, sir_inside, evals, iters, lin_fail_zero, lin_fail_q, lin_fail_tie, lin_fail_zone, lit_adds;
 };
 static Prof g_prof;
 #define PT_MPROF(f) (g_prof.f++)
@@ -225,6 +225,7 @@ int main(int argc, char **argv) {
                (double)g_prof.sir_inside / n, dt / n * 1e6);
         printf("hit jobs: iters %.2f tries %.2f   miss jobs: iters %.2f tries %.2f\n", hit_it / nh, hit_tries / nh,
                miss_it / nm, miss_tries / nm);
+        printf("advance literal adds per job %.2f\n", (double)g_prof.lit_adds / n);
         printf("lin_init fails per job: zero %.2f q %.2f tie %.2f zone %.2f\n", (double)g_prof.lin_fail_zero / n,
                (double)g_prof.lin_fail_q / n, (double)g_prof.lin_fail_tie / n, (double)g_prof.lin_fail_zone / n);
         if (argc > 4) {  // results for device comparisons: t, hit, iterations per job

@@ -172,8 +172,9 @@ PT_HD double lin_at(const Lin &L, double x, int64_t j) {
 // the same (X, R, u) wherever lin_init's room is >= 2, which is all its callers
 // use.  floor(span / step) needs one correction each way: span / step < 2^41
 // and the polished reciprocal is good to a few ulp, so the estimate is off by
-// less than 1.
-PT_HD double lin_room(double x, double c, Lin *L) {
+// less than 1.  need: a room of at least `need` comes back as `need` without
+// the division (the callers take min(room, need)).
+PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
     PT_MPROF(lin_init);
     const double ax = fabs(x), ac = fabs(c);
     const bool ok0 = x != 0.0 && ax < 1e300 && ac < 1e300;  // zero, inf, NaN: no
@@ -181,9 +182,11 @@ PT_HD double lin_room(double x, double c, Lin *L) {
     const double sc = ldexp(1.0, 52 - e);  // 1/u, a power of two: scaling by it is exact
     const double q = c * sc, X = x * sc, aq = fabs(q);
     const double qf = floor(q);
-    const bool tie = q - qf == 0.5;  // round-half-even: only from an even X (then R is the even neighbour)
+    const bool tie = q - qf == 0.5;  // round-half-even: only from an even X
     const bool xodd = floor(X * 0.5) * 2.0 != X;
-    const double R = tie ? (floor(qf * 0.5) * 2.0 == qf ? qf : qf + 1.0) : rint(q);
+    // rint rounds half to even: on a tie it is the even one of qf, qf + 1,
+    // the step a sum from an even X takes
+    const double R = rint(q);
     const double C = ceil(aq);
     const double lo = 4503599627370496.0 + C + 1.0, hi = 9007199254740992.0 - C - 1.0;
     const double A = fabs(X), Rs = X >= 0.0 ? R : -R;
@@ -194,10 +197,19 @@ PT_HD double lin_room(double x, double c, Lin *L) {
     L->u = ldexp(1.0, e - 52);
     L->frozen = c == 0.0;
     const double span = Rs > 0.0 ? hi - A : A - lo, step = fabs(Rs);
-    double k = floor(span * approx_rcp(step));
-    k = k * step > span ? k - 1.0 : k;
-    k = (k + 1.0) * step <= span ? k + 1.0 : k;
-    const double room = Rs == 0.0 || span >= BIGD * step ? BIGD : k + 1.0;
+    double room;
+    if (Rs == 0.0 || span >= BIGD * step) {
+        room = BIGD;
+    } else if ((need - 1.0) * step <= span) {
+        // the caller's `need` steps fit (room = floor(span / step) + 1 >= need;
+        // the product is exact below 2^53 and above span otherwise): no division
+        room = need;
+    } else {
+        double k = floor(span * approx_rcp(step));
+        k = k * step > span ? k - 1.0 : k;
+        k = (k + 1.0) * step <= span ? k + 1.0 : k;
+        room = k + 1.0;
+    }
     if (c == 0.0) return BIGD;
     return ok ? room : 0.0;
 }
@@ -232,7 +244,7 @@ PT_HD double advance(double x, double c, double n) {
         }
         PT_MPROF(advance_loops);
         Lin L;
-        const double room = lin_room(x, c, &L);
+        const double room = lin_room(x, c, &L, n);
         // the closed form to the end of the segment (or n), then the literal
         // add that leaves it; a literal add alone in an edge zone
         const double k = room >= 2.0 ? (room < n ? room : n) : 0.0;
@@ -256,7 +268,7 @@ PT_HD void seg_step(double &x, double c, double &n) {
         return;
     }
     Lin L;
-    const double room = lin_room(x, c, &L);
+    const double room = lin_room(x, c, &L, n);
     const double k = room >= 2.0 ? (room < n ? room : n) : 0.0;
     if (k > 0.0) x = L.frozen ? x : (L.X + k * L.R) * L.u;
     n -= k;

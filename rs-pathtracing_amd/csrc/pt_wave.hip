@@ -1250,12 +1250,23 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // runs beside the other chunk's compaction and march (VALU-bound) instead
     // of both chunks bouncing, then both marching, at the same time.
     struct Chunk {
-        uint32_t g0, gt, s0;
+        uint32_t g0, gt, s0, ns;
     };
+    // Sample chunks of a tile group: as few as fit ns samples each, rounded up
+    // to whole rounds of `slots` (no round with an idle stream), with the
+    // samples spread evenly over them (no short last chunk).  The per-pixel
+    // sums take the chunks in sample order either way.
+    uint32_t nchunks = (P0.spp + ns - 1) / ns;
+    if (slots > 1 && nchunks > 1 && nchunks % (uint32_t)slots) nchunks += (uint32_t)slots - nchunks % (uint32_t)slots;
+    if (nchunks > P0.spp) nchunks = P0.spp;
     std::vector<Chunk> chunk_list;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        for (uint32_t s0 = 0; s0 < P0.spp; s0 += ns) chunk_list.push_back(Chunk{g0, gt, s0});
+        for (uint32_t c = 0, s0 = 0; c < nchunks; c++) {
+            const uint32_t n = P0.spp / nchunks + (c < P0.spp % nchunks ? 1u : 0u);  // <= ns
+            chunk_list.push_back(Chunk{g0, gt, s0, n});
+            s0 += n;
+        }
     }
     // wf_pingpong bit 0: chain the bounce launches; bit 1: chain the march launches
     const bool pingpong = (tu.wf_pingpong & 1) && slots > 1, mchain = (tu.wf_pingpong & 2) && slots > 1;
@@ -1269,7 +1280,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             v.tile0 = P0.tile_begin + ch.g0;
             v.npix = ch.gt * TILE * TILE;
             v.s0 = ch.s0;
-            v.ns = P0.spp - ch.s0 < ns ? P0.spp - ch.s0 : ns;
+            v.ns = ch.ns;
             const uint32_t paths = v.ns * v.npix;
             (void)paths;  // (every bounce writes the status of each of its inputs; compaction reads no further)
             if ((e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;

@@ -423,6 +423,11 @@ def main():
                 rec["roofline"]["traffic"] = round(kind["traffic"])
                 rec["roofline"]["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % tf.relative_to(ROOT)
                 rec["roofline"]["traffic_gbs"] = round(kind["traffic"] / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
+                # per sample, independent of the chunk size (bytes per launch scale with the paths per chunk)
+                rec["roofline"]["traffic_per_sample"] = round(kind["traffic"] * dom_n / (W * H * spp), 1)
+                if kind.get("launches") not in (None, dom_n):
+                    rec["roofline"]["traffic_note"] = "PMC file launches %s != %d launches per frame here" % (
+                        kind["launches"], dom_n)
         if not args.no_parity:
             import oracle
             px = parity_pixels(args)

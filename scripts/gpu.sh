@@ -60,7 +60,7 @@ evidence)
     bash scripts/gpu.sh smoke $tag
     bash scripts/gpu.sh bench $tag
     bash scripts/gpu.sh kt $tag/kt_default --no-cpu-baseline --no-parity
-    bash scripts/gpu.sh kt $tag/kt_one_stream --slots 1 --no-cpu-baseline --no-parity --no-roofline-leg ;;
+    KT_FRAMES=4 bash scripts/gpu.sh kt $tag/kt_one_stream --slots 1 --no-cpu-baseline --no-parity --no-roofline-leg ;;
 *)
     echo "usage: scripts/gpu.sh tests|smoke|bench|kt|pmc|sq|evidence <tag> [args]"; exit 2 ;;
 esac

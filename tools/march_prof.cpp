@@ -200,7 +200,20 @@ int main(int argc, char **argv) {
             uint32_t tr0 = ms.tries;
             int stt;
             long guard = 0;
-            while ((stt = march::march_step<true>(m, &ms)) == march::M_RUNNING) {
+#ifndef PROF_EXTADV
+#define PROF_EXTADV 0  // 1: the block advance done by the caller after the iteration (wf_march's coop_advance)
+#endif
+            while ((stt = march::march_step<true, PROF_EXTADV == 0>(m, &ms)) == march::M_RUNNING) {
+                if (PROF_EXTADV && m.adv) {
+                    const double s = m.s, g = m.na[0];
+                    m.t = march::advance(m.t, s, g);
+                    m.px = march::advance(m.px, m.dx * s, g);
+                    m.py = march::advance(m.py, m.dy * s, g);
+                    m.pz = march::advance(m.pz, m.dz * s, g);
+                    m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
+                    m.adv = 0;
+                    m.r = march::shape_f_k<march::F_HEART>(m.F, m.px, m.py, m.pz);
+                }
                 if (++guard > 2000000) {
                     printf("RUNAWAY job %zu: step %.17g passes %d o %.17g %.17g %.17g d %.17g %.17g %.17g  t %.17g s %.17g pass %d lim %lld r %.17g\n",
                            i, q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], m.t, m.s, m.pass,

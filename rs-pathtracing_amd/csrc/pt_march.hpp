@@ -221,6 +221,9 @@ PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
 // closed-form segment costs ~150 instructions against ~5 per literal add: C2
 // one-stream march 183 -> 172 ms).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
+#ifndef PT_ADV_PEEL
+#define PT_ADV_PEEL 1  // a proven block's four advances start with one straight-line segment each
+#endif
 #ifndef PT_ADV_NZB
 #define PT_ADV_NZB 4  // literal adds per trip in the near-zero zone
 #endif
@@ -809,10 +812,25 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     // one loop per coordinate: a lane pays only for the binade
                     // segments each coordinate actually crosses
                     PT_MREG(adv_begin);
+#if PT_ADV_PEEL
+                    // every coordinate's first segment side by side (four
+                    // independent chains), then the rest for those that cross
+                    // binade edges
+                    double n0 = good, n1 = good, n2 = good, n3 = good;
+                    seg_step(m.t, s, n0);
+                    seg_step(m.px, cx, n1);
+                    seg_step(m.py, cy, n2);
+                    seg_step(m.pz, cz, n3);
+                    if (n0 > 0.0) m.t = advance(m.t, s, n0);
+                    if (n1 > 0.0) m.px = advance(m.px, cx, n1);
+                    if (n2 > 0.0) m.py = advance(m.py, cy, n2);
+                    if (n3 > 0.0) m.pz = advance(m.pz, cz, n3);
+#else
                     m.t = advance(m.t, s, good);
                     m.px = advance(m.px, cx, good);
                     m.py = advance(m.py, cy, good);
                     m.pz = advance(m.pz, cz, good);
+#endif
                     m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
                     m.adv = 0;
                     m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);

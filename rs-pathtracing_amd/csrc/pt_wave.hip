@@ -357,7 +357,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             PT_BSTAMP(5)
             if (need_march || b + 1 >= PT_WF_BPL) break;
         }
-        if (live) store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+#ifndef PT_WF_STORE_ALL
+#define PT_WF_STORE_ALL 1  // every input position's state is written (ended paths too: whole lines)
+#endif
+        if (live || (PT_WF_STORE_ALL && i < count))
+            store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
         if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
     }

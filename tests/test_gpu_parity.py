@@ -235,6 +235,10 @@ def test_wavefront_chunks_and_tile_groups(pt, cornell):
     for slots in (1, 3):
         img, ref = render_pair(pt, cornell, 70, 45, 2, 8, seed=10, wf_paths=256 * 7, wf_slots=slots)
         check_image(img, ref)
+    # uneven sample chunks: 6 tiles, 2 spp per chunk at most, 5 spp -> 3 chunks,
+    # rounded up to 4 for two streams and balanced to 2, 1, 1, 1 samples
+    img, ref = render_pair(pt, cornell, 37, 21, 5, 8, seed=12, wf_paths=256 * 6 * 2, wf_slots=2)
+    check_image(img, ref)
 
 
 def test_wavefront_deep_paths(pt, spheres, cornell):

@@ -181,22 +181,22 @@ PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
     const int e = ilogb(ok0 ? x : 1.0);
     const double sc = ldexp(1.0, 52 - e);  // 1/u, a power of two: scaling by it is exact
     const double q = c * sc, X = x * sc, aq = fabs(q);
-    const double qf = floor(q);
-    const bool tie = q - qf == 0.5;  // round-half-even: only from an even X
-    const bool xodd = floor(X * 0.5) * 2.0 != X;
-    // rint rounds half to even: on a tie it is the even one of qf, qf + 1,
-    // the step a sum from an even X takes
+    // rint rounds half to even: on a tie it is the even one of floor(q) and
+    // floor(q) + 1, the step a sum from an even X takes (q - R is exact)
     const double R = rint(q);
+    const bool tie = fabs(q - R) == 0.5;  // round-half-even: only from an even X
+    const bool xodd = (f64_to_bits(x) & 1u) != 0;  // X's parity is x's last mantissa bit (x normal)
     const double C = ceil(aq);
     const double lo = 4503599627370496.0 + C + 1.0, hi = 9007199254740992.0 - C - 1.0;
     const double A = fabs(X), Rs = X >= 0.0 ? R : -R;
-    const bool zone = Rs > 0.0 ? A > hi : (Rs < 0.0 && A < lo);
-    const bool ok = ok0 && e >= -960 && aq < 4.0e15 && !(tie && xodd) && !zone;
     L->X = X;
     L->R = R;
     L->u = ldexp(1.0, e - 52);
     L->frozen = c == 0.0;
+    // grid steps to the edge the sequence moves toward (negative: already past it)
     const double span = Rs > 0.0 ? hi - A : A - lo, step = fabs(Rs);
+    const bool zone = Rs != 0.0 && span < 0.0;
+    const bool ok = ok0 && e >= -960 && aq < 4.0e15 && !(tie && xodd) && !zone;
     double room;
     if (Rs == 0.0 || span >= BIGD * step) {
         room = BIGD;

@@ -178,9 +178,15 @@ PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
     PT_MPROF(lin_init);
     const double ax = fabs(x), ac = fabs(c);
     const bool ok0 = x != 0.0 && ax < 1e300 && ac < 1e300;  // zero, inf, NaN: no
+#if defined(__HIP_DEVICE_COMPILE__)
+    // v_frexp_exp: ilogb for finite nonzero x (0, inf, NaN give a value the ok
+    // test below masks), without libm's special-case selects
+    const int e = __builtin_amdgcn_frexp_exp(x) - 1;
+#else
     const int e = ilogb(ok0 ? x : 1.0);
-    const double sc = ldexp(1.0, 52 - e);  // 1/u, a power of two: scaling by it is exact
-    const double q = c * sc, X = x * sc, aq = fabs(q);
+#endif
+    // X = x / u, q = c / u: scaling by a power of two is exact (ldexp: no multiply)
+    const double q = ldexp(c, 52 - e), X = ldexp(x, 52 - e), aq = fabs(q);
     // rint rounds half to even: on a tie it is the even one of floor(q) and
     // floor(q) + 1, the step a sum from an even X takes (q - R is exact)
     const double R = rint(q);

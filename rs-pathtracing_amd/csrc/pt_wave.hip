@@ -92,12 +92,23 @@ using dev::V3;
 // alternate by iteration), so every later kernel reads a dense, id-ordered
 // subsequence of the previous bounce's outputs instead of a sparse one of the
 // chunk's slots.  The slot id (sample, pixel) travels with the path.
+// One base pointer and the slot count (not 11 pointers): the kernels' two
+// sets would otherwise hold 44 SGPRs of addresses.
 struct PathSoA {
-    double *ox, *oy, *oz, *dx, *dy, *dz, *t;  // ray, best hit t
-    uint64_t *rng;
-    int32_t *who;    // best hit shape (-1: miss)
-    uint32_t *meta;  // depth | stack count << 8
-    uint32_t *sid;   // slot id of the path
+    char *base;
+    size_t cap;
+    static constexpr size_t BYTES = 8 * 8 + 3 * 4;  // per path
+    __host__ __device__ double *ox() const { return (double *)base; }  // ray, best hit t
+    __host__ __device__ double *oy() const { return (double *)base + cap; }
+    __host__ __device__ double *oz() const { return (double *)base + 2 * cap; }
+    __host__ __device__ double *dx() const { return (double *)base + 3 * cap; }
+    __host__ __device__ double *dy() const { return (double *)base + 4 * cap; }
+    __host__ __device__ double *dz() const { return (double *)base + 5 * cap; }
+    __host__ __device__ double *t() const { return (double *)base + 6 * cap; }
+    __host__ __device__ uint64_t *rng() const { return (uint64_t *)base + 7 * cap; }
+    __host__ __device__ int32_t *who() const { return (int32_t *)((double *)base + 8 * cap); }  // best hit shape (-1: miss)
+    __host__ __device__ uint32_t *meta() const { return (uint32_t *)((double *)base + 8 * cap) + cap; }  // depth | stack count << 8
+    __host__ __device__ uint32_t *sid() const { return (uint32_t *)((double *)base + 8 * cap) + 2 * cap; }  // slot id of the path
 };
 
 // Device view of the workspace for one chunk.
@@ -197,17 +208,17 @@ __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const Mem
 // A live path's state at output position k.
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
                                            int who, uint64_t rng, uint32_t meta) {
-    S.ox[k] = ray.o.x;
-    S.oy[k] = ray.o.y;
-    S.oz[k] = ray.o.z;
-    S.dx[k] = ray.d.x;
-    S.dy[k] = ray.d.y;
-    S.dz[k] = ray.d.z;
-    S.t[k] = best;
-    S.who[k] = who;
-    S.rng[k] = rng;
-    S.meta[k] = meta;
-    S.sid[k] = id;
+    S.ox()[k] = ray.o.x;
+    S.oy()[k] = ray.o.y;
+    S.oz()[k] = ray.o.z;
+    S.dx()[k] = ray.d.x;
+    S.dy()[k] = ray.d.y;
+    S.dz()[k] = ray.d.z;
+    S.t()[k] = best;
+    S.who()[k] = who;
+    S.rng()[k] = rng;
+    S.meta()[k] = meta;
+    S.sid()[k] = id;
 }
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
@@ -285,13 +296,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
                 const PathSoA &S = v.in;
-                id = S.sid[p];
-                ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
-                ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
-                rng.s = S.rng[p];
-                const uint32_t meta = S.meta[p];
-                who = S.who[p];
-                best = S.t[p];
+                id = S.sid()[p];
+                ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
+                ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
+                rng.s = S.rng()[p];
+                const uint32_t meta = S.meta()[p];
+                who = S.who()[p];
+                best = S.t()[p];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
@@ -427,17 +438,17 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
             } else {
                 const uint32_t p = v.list[k];
                 const PathSoA &S = v.in;
-                id = S.sid[p];
-                ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
-                ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
-                rng.s = S.rng[p];
-                const uint32_t meta = S.meta[p];
+                id = S.sid()[p];
+                ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
+                ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
+                rng.s = S.rng()[p];
+                const uint32_t meta = S.meta()[p];
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 if (EXT) stk.vb = v.att + id;
-                who = S.who[p];
-                best = S.t[p];
+                who = S.who()[p];
+                best = S.t()[p];
             }
         }
         if (!done && shade_now) {
@@ -659,10 +670,10 @@ struct MarchJob {
 
 __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob *j) {
     j->id = p;
-    j->ray.o = dev::v3(S.ox[p], S.oy[p], S.oz[p]);
-    j->ray.d = dev::v3(S.dx[p], S.dy[p], S.dz[p]);
-    j->best = S.t[p];
-    j->who = S.who[p];
+    j->ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
+    j->ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
+    j->best = S.t()[p];
+    j->who = S.who()[p];
 }
 
 // DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
@@ -724,8 +735,8 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         const uint32_t id = mq[k];  // position in the bounce's output
         if (pre) {
             cur.id = id;
-            cur.best = v.out.t[id];
-            cur.who = v.out.who[id];
+            cur.best = v.out.t()[id];
+            cur.who = v.out.who()[id];
             const double2 *j = v.jo + (size_t)id * 4;
             const double2 a = j[0], b = j[1], c = j[2], e = j[3];
             march::march_start<FK>(F0, step0, passes0, a.x, a.y, b.x, b.y, c.x, c.y, e.x, e.y, &ms);
@@ -843,15 +854,15 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 const double fbest = cur.best;
                 const int fwho = cur.who;
                 if (!PT_WF_STORE_LATE) {
-                    v.out.t[fid] = fbest;
-                    v.out.who[fid] = fwho;
+                    v.out.t()[fid] = fbest;
+                    v.out.who()[fid] = fwho;
                 }
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
                 if (have) start_job(pos(q));
                 if (PT_WF_STORE_LATE) {
-                    v.out.t[fid] = fbest;
-                    v.out.who[fid] = fwho;
+                    v.out.t()[fid] = fbest;
+                    v.out.who()[fid] = fwho;
                 }
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
@@ -1179,7 +1190,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // pre-selected march jobs: one marched shape, PT_WF_PRESELECT
     const bool presel = PT_WF_PRESELECT && sc.nmarch == 1 && !ws->diag;
     // two path-state sets (8 + 3 words per path each), sample radiances, lists, end depths
-    const size_t slot_bytes = al((size_t)cap * 8) * 19 + (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 9 +
+    const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 8) * 3 +
+                              (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 3 +
                               al((size_t)cap * 4 * (P0.depth + 1)) +
                               al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 12) + al(cnt_words * 4) +
                               al(att_bytes);
@@ -1198,17 +1210,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         WfView &v = sl[k].v;
         for (int h = 0; h < 2; h++) {
             PathSoA &S = sl[k].set[h];
-            S.ox = (double *)take((size_t)cap * 8);
-            S.oy = (double *)take((size_t)cap * 8);
-            S.oz = (double *)take((size_t)cap * 8);
-            S.dx = (double *)take((size_t)cap * 8);
-            S.dy = (double *)take((size_t)cap * 8);
-            S.dz = (double *)take((size_t)cap * 8);
-            S.t = (double *)take((size_t)cap * 8);
-            S.rng = (uint64_t *)take((size_t)cap * 8);
-            S.who = (int32_t *)take((size_t)cap * 4);
-            S.meta = (uint32_t *)take((size_t)cap * 4);
-            S.sid = (uint32_t *)take((size_t)cap * 4);
+            S.base = (char *)take((size_t)cap * PathSoA::BYTES);
+            S.cap = cap;
         }
         v.fin = (uint32_t *)take((size_t)cap * 4);
         v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));

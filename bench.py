@@ -104,6 +104,9 @@ def parse():
                     help="a renderer tuning option (pt_renderer_set_option), repeatable")
     ap.add_argument("--single-process", action="store_true",
                     help="N GPUs behind one renderer (pt_renderer_create_multi, peer-copy gather) instead of ranks")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="ranks' process group: nccl (= RCCL, the multi-GPU default) or gloo (rehearsal: shards "
+                         "gathered through host memory, ranks may share a GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of each CPU-baseline run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -237,9 +240,15 @@ def main():
     multi = args.single_process and world == 1 and args.gpus > 1
     if world != args.gpus and rank == 0 and not multi:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    gloo = world > 1 and args.dist_backend == "gloo"
+    if gloo:  # rehearsal of the multi-rank path on fewer GPUs than ranks
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import __graft_entry__ as ge
     pt = ge.load_package()
@@ -267,7 +276,11 @@ def main():
     if world > 1:
         shard = torch.zeros(per * 256 * 3, dtype=torch.float64, device="cuda")
         gathered = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda") if rank == 0 else None
-        glist = list(gathered.view(world, -1).unbind(0)) if rank == 0 else None
+        if gloo:  # gloo gathers host tensors
+            shard_h = torch.zeros(shard.numel(), dtype=torch.float64)
+            gathered_h = torch.zeros(gathered.numel(), dtype=torch.float64) if rank == 0 else None
+        g = gathered_h if gloo else gathered
+        glist = list(g.view(world, -1).unbind(0)) if rank == 0 else None
     torch.cuda.synchronize()
 
     k_start, k_end = [], []
@@ -285,7 +298,13 @@ def main():
         k_start.append(ev0)
         k_end.append(ev1)
         if world > 1:
-            dist.gather(shard, glist, dst=0)
+            if gloo:
+                shard_h.copy_(shard)  # synchronous D2H on the render stream
+                dist.gather(shard_h, glist, dst=0)
+                if rank == 0:
+                    gathered.copy_(gathered_h)
+            else:
+                dist.gather(shard, glist, dst=0)
             if rank == 0:
                 pt.unshard_device(gathered.data_ptr(), W, H, world, frame.data_ptr(), sp, device=local)
 
@@ -310,7 +329,7 @@ def main():
     guard_drops = pt.march_guard_drops(r)
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms_max = t.tolist()
     else:
@@ -382,6 +401,8 @@ def main():
             "config": {"workload": workload, "config": args.config or ("c2" if metric_name(args) == METRIC else None),
                        "width": W, "height": H, "spp": spp, "depth": args.depth, "seed": args.seed,
                        "parallelism": ("%d devices in one process, peer-copy gather" % args.gpus if multi else
+                                       "tile-interleaved x%d, gloo gather through host memory (rehearsal, %d "
+                                       "GPU(s))" % (world, torch.cuda.device_count()) if gloo else
                                        "tile-interleaved x%d, RCCL gather" % world if world > 1 else "single GPU"),
                        "wf_slots": slots},
             "roofline": {"bound": "valu_f64", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,

@@ -205,20 +205,30 @@ __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const Mem
     v.fin[id] = (uint32_t)stk.n;
 }
 
-// A live path's state at output position k.
+// A live path's state at output position k.  PT_WF_NT: non-temporal stores
+// (the state is read back only by the next bounce, after 1.8 GB of other
+// traffic: no cache level holds it that long).
+#ifndef PT_WF_NT
+#define PT_WF_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void st_path(T *p, T x) {
+    if (PT_WF_NT) __builtin_nontemporal_store(x, p);
+    else *p = x;
+}
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
                                            int who, uint64_t rng, uint32_t meta) {
-    S.ox()[k] = ray.o.x;
-    S.oy()[k] = ray.o.y;
-    S.oz()[k] = ray.o.z;
-    S.dx()[k] = ray.d.x;
-    S.dy()[k] = ray.d.y;
-    S.dz()[k] = ray.d.z;
-    S.t()[k] = best;
-    S.who()[k] = who;
-    S.rng()[k] = rng;
-    S.meta()[k] = meta;
-    S.sid()[k] = id;
+    st_path(S.ox() + k, ray.o.x);
+    st_path(S.oy() + k, ray.o.y);
+    st_path(S.oz() + k, ray.o.z);
+    st_path(S.dx() + k, ray.d.x);
+    st_path(S.dy() + k, ray.d.y);
+    st_path(S.dz() + k, ray.d.z);
+    st_path(S.t() + k, best);
+    st_path(S.who() + k, (int32_t)who);
+    st_path(S.rng() + k, (uint64_t)rng);
+    st_path(S.meta() + k, meta);
+    st_path(S.sid() + k, id);
 }
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
@@ -581,54 +591,100 @@ __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, 
 }
 
 // one block: exclusive scan of the tile counts in place; totals go to the
-// counters the next kernels read (n_long: where the short march jobs start)
+// counters the next kernels read (n_long: where the short march jobs start).
+// Each thread owns a contiguous run of tiles, loaded into registers up front
+// (every load in flight together), and the block scans once, not once per 256
+// tiles.  Runs longer than SCAN_RUN (more than 8192 tiles: chunks over 33M
+// paths) take the loop.
+constexpr int SCAN_RUN = 32;
 __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, uint32_t *__restrict__ n_live,
                                                uint32_t *__restrict__ n_march, uint32_t *__restrict__ n_long) {
     __shared__ uint32_t lds[12];
-    uint32_t cl = 0, cg = 0, cs = 0;
-    for (uint32_t b0 = 0; b0 < nblk; b0 += blockDim.x) {
-        const uint32_t b = b0 + threadIdx.x;
-        const uint32_t l = b < nblk ? blk[3 * b] : 0u, g = b < nblk ? blk[3 * b + 1] : 0u,
-                       h = b < nblk ? blk[3 * b + 2] : 0u;
-        uint32_t tl, tg, ts;
-        const uint32_t el = block_exscan(l, &tl, lds), eg = block_exscan(g, &tg, lds + 4),
-                       es = block_exscan(h, &ts, lds + 8);
-        if (b < nblk) {
-            blk[3 * b] = cl + el;
-            blk[3 * b + 1] = cg + eg;
-            blk[3 * b + 2] = cs + es;
+    const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    uint32_t sl = 0, sg = 0, ss = 0, tl, tg, ts;
+    if (per <= (uint32_t)SCAN_RUN) {  // (block-uniform)
+        uint32_t rl[SCAN_RUN], rg[SCAN_RUN], rs[SCAN_RUN];
+#pragma unroll
+        for (int j = 0; j < SCAN_RUN; j++) {
+            const uint32_t b = b0 + j;
+            const bool ok = b < b1;
+            rl[j] = ok ? blk[3 * b] : 0u;
+            rg[j] = ok ? blk[3 * b + 1] : 0u;
+            rs[j] = ok ? blk[3 * b + 2] : 0u;
         }
-        cl += tl;
-        cg += tg;
-        cs += ts;
+#pragma unroll
+        for (int j = 0; j < SCAN_RUN; j++) sl += rl[j], sg += rg[j], ss += rs[j];
+        uint32_t cl = block_exscan(sl, &tl, lds), cg = block_exscan(sg, &tg, lds + 4), cs = block_exscan(ss, &ts, lds + 8);
+#pragma unroll
+        for (int j = 0; j < SCAN_RUN; j++) {
+            const uint32_t b = b0 + j;
+            if (b < b1) {
+                blk[3 * b] = cl;
+                blk[3 * b + 1] = cg;
+                blk[3 * b + 2] = cs;
+            }
+            cl += rl[j];
+            cg += rg[j];
+            cs += rs[j];
+        }
+    } else {
+        for (uint32_t b = b0; b < b1; b++) {
+            sl += blk[3 * b];
+            sg += blk[3 * b + 1];
+            ss += blk[3 * b + 2];
+        }
+        uint32_t cl = block_exscan(sl, &tl, lds), cg = block_exscan(sg, &tg, lds + 4), cs = block_exscan(ss, &ts, lds + 8);
+        for (uint32_t b = b0; b < b1; b++) {
+            const uint32_t l = blk[3 * b], g = blk[3 * b + 1], h = blk[3 * b + 2];
+            blk[3 * b] = cl;
+            blk[3 * b + 1] = cg;
+            blk[3 * b + 2] = cs;
+            cl += l;
+            cg += g;
+            cs += h;
+        }
     }
     if (threadIdx.x == 0) {
-        *n_live = cl;
-        *n_march = cg + cs;
-        *n_long = cg;
+        *n_live = tl;
+        *n_march = tg + ts;
+        *n_long = tg;
     }
 }
 
+// The tile's ids are compacted into LDS first (in order), then copied out
+// with consecutive lanes on consecutive positions (one thread's 16 statuses
+// scattered straight to HBM would touch 64 lines per wave store).
 __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st, const uint32_t *__restrict__ blk,
                                                   const uint32_t *__restrict__ n_long, uint32_t *__restrict__ live_out,
                                                   uint32_t *__restrict__ march_out, const uint32_t *__restrict__ n_dev,
                                                   uint32_t n_host) {
     __shared__ uint32_t lds[12];
+    __shared__ uint32_t ids[CP_TILE];  // the tile's live ids, then its march ids (long, then short)
     const size_t base = (size_t)blockIdx.x * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
     const uint4 q = cp_load(st, n_dev, n_host);
     uint32_t l, m, g, tl, tg, ts;
     cp_bits(q, &l, &m, &g);
-    uint32_t ol = blk[3 * blockIdx.x] + block_exscan(l, &tl, lds);
-    uint32_t og = blk[3 * blockIdx.x + 1] + block_exscan(g, &tg, lds + 4);
-    uint32_t os = *n_long + blk[3 * blockIdx.x + 2] + block_exscan(m - g, &ts, lds + 8);
+    uint32_t ol = block_exscan(l, &tl, lds);
+    uint32_t og = block_exscan(g, &tg, lds + 4);
+    uint32_t os = tg + block_exscan(m - g, &ts, lds + 8);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < CP_ITEMS; k++)
+        if ((w[k >> 2] >> (8 * (k & 3))) & 1u) ids[ol++] = (uint32_t)(base + k);
+    __syncthreads();
+    const uint32_t bl = blk[3 * blockIdx.x], bg = blk[3 * blockIdx.x + 1], bs = *n_long + blk[3 * blockIdx.x + 2];
+    for (uint32_t k = threadIdx.x; k < tl; k += CP_BLOCK) live_out[bl + k] = ids[k];
+    if (tg + ts == 0) return;  // (block-uniform)
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < CP_ITEMS; k++) {
         const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        const uint32_t id = (uint32_t)(base + k);
-        if (b & 1u) live_out[ol++] = id;
-        if (b & 2u) march_out[(b & 4u) ? og++ : os++] = id;
+        if (b & 2u) ids[(b & 4u) ? og++ : os++] = (uint32_t)(base + k);
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < tg; k += CP_BLOCK) march_out[bg + k] = ids[k];
+    for (uint32_t k = threadIdx.x; k < ts; k += CP_BLOCK) march_out[bs + k] = ids[tg + k];
 }
 
 // Marches of iteration `it`.  Each workgroup owns a contiguous slice of the

@@ -198,7 +198,17 @@ __device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3
 // and its attenuation-stack depth; the per-pixel reduce unwinds the stack
 // (the recursion's products, in its order) when it sums the chunk's samples,
 // so the bounce kernel's waves never wait for the unwind's dependent loads.
+#ifndef PT_WF_NT_END
+#define PT_WF_NT_END 1  // non-temporal too (read once, by the chunk's reduce): iso bounce -0.6 ms, C2 +0.4 %
+#endif
 __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const MemStack &stk, V3 leaf) {
+    if (PT_WF_NT_END) {
+        __builtin_nontemporal_store(leaf.x, v.rx + id);
+        __builtin_nontemporal_store(leaf.y, v.ry + id);
+        __builtin_nontemporal_store(leaf.z, v.rz + id);
+        __builtin_nontemporal_store((uint32_t)stk.n, v.fin + id);
+        return;
+    }
     v.rx[id] = leaf.x;
     v.ry[id] = leaf.y;
     v.rz[id] = leaf.z;
@@ -209,12 +219,20 @@ __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const Mem
 // (the state is read back only by the next bounce, after 1.8 GB of other
 // traffic: no cache level holds it that long).
 #ifndef PT_WF_NT
-#define PT_WF_NT 0
+#define PT_WF_NT 1  // C2: iso bounce 216.2 -> 211.5 ms, 1792 -> 1814 M samples/s (non-temporal loads: slower)
 #endif
 template <typename T>
 __device__ __forceinline__ void st_path(T *p, T x) {
     if (PT_WF_NT) __builtin_nontemporal_store(x, p);
     else *p = x;
+}
+#ifndef PT_WF_NTL
+#define PT_WF_NTL 0  // non-temporal path-state loads in the bounce kernel
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_path(const T *p) {
+    if (PT_WF_NTL) return __builtin_nontemporal_load(p);
+    return *p;
 }
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
                                            int who, uint64_t rng, uint32_t meta) {
@@ -306,13 +324,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
                 const PathSoA &S = v.in;
-                id = S.sid()[p];
-                ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
-                ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
-                rng.s = S.rng()[p];
-                const uint32_t meta = S.meta()[p];
-                who = S.who()[p];
-                best = S.t()[p];
+                id = ld_path(S.sid() + p);
+                ray.o = dev::v3(ld_path(S.ox() + p), ld_path(S.oy() + p), ld_path(S.oz() + p));
+                ray.d = dev::v3(ld_path(S.dx() + p), ld_path(S.dy() + p), ld_path(S.dz() + p));
+                rng.s = ld_path(S.rng() + p);
+                const uint32_t meta = ld_path(S.meta() + p);
+                who = ld_path(S.who() + p);
+                best = ld_path(S.t() + p);
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
@@ -354,11 +372,23 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
                 if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
-                    double2 *j = v.jo + (size_t)i * 4;
-                    j[0] = make_double2(o.x, o.y);
-                    j[1] = make_double2(o.z, d.x);
-                    j[2] = make_double2(d.y, d.z);
-                    j[3] = make_double2(st, en);
+                    if (!PT_WF_NT) {
+                        double2 *j = v.jo + (size_t)i * 4;
+                        j[0] = make_double2(o.x, o.y);
+                        j[1] = make_double2(o.z, d.x);
+                        j[2] = make_double2(d.y, d.z);
+                        j[3] = make_double2(st, en);
+                    } else {
+                    double *j = (double *)(v.jo + (size_t)i * 4);
+                    st_path(j + 0, o.x);
+                    st_path(j + 1, o.y);
+                    st_path(j + 2, o.z);
+                    st_path(j + 3, d.x);
+                    st_path(j + 4, d.y);
+                    st_path(j + 5, d.z);
+                    st_path(j + 6, st);
+                    st_path(j + 7, en);
+                    }
                     // queue order only: a march that will cross the surface (a hit: ~3x
                     // the iterations of a miss) is predicted by the sign of f at the bound
                     // entry and at PT_WF_PREDICT points along the chord (inside is f < 0;

@@ -45,7 +45,7 @@ struct Tuning {
     int mega_waves = 4;              // PT_WAVES: megakernel register budget, waves per SIMD (2..5)
     int diag = 0;                    // PT_DIAG bit 0: skip ray-marched shapes (a timing ablation, not the reference)
     int wf_slots = 2;                // PT_WF_SLOTS: sample chunks in flight, one stream each (1..4)
-    int64_t wf_paths = 3 << 23;      // PT_WF_PATHS: path slots per chunk (256 .. 2^28); 24M: 12 spp of 1080p
+    int64_t wf_paths = 3 << 24;      // PT_WF_PATHS: path slots per chunk (256 .. 2^28); 48M: 24 spp of 1080p (24M: 1795, 32M: 1818, 48M: 1830, 64M: 1832 M samples/s)
     int wf_min_chunks = 1;           // PT_WF_MIN_CHUNKS: at least this many sample chunks per frame (1..4096)
     int wf_bounce_waves = 3;         // PT_WF_BOUNCE_WAVES: wf_bounce register budget (2, 3, 4, 5, 6, 8)
     int wf_fused = 0;                // PT_WF_FUSED: fused bounces (wf_trace) instead of one launch per bounce

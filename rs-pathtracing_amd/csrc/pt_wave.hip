@@ -659,12 +659,14 @@ __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint3
             cs += rs[j];
         }
     } else {
+#pragma unroll 8
         for (uint32_t b = b0; b < b1; b++) {
             sl += blk[3 * b];
             sg += blk[3 * b + 1];
             ss += blk[3 * b + 2];
         }
         uint32_t cl = block_exscan(sl, &tl, lds), cg = block_exscan(sg, &tg, lds + 4), cs = block_exscan(ss, &ts, lds + 8);
+#pragma unroll 8
         for (uint32_t b = b0; b < b1; b++) {
             const uint32_t l = blk[3 * b], g = blk[3 * b + 1], h = blk[3 * b + 2];
             blk[3 * b] = cl;
@@ -737,6 +739,9 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 #endif
 #ifndef PT_WF_BOUNCE_CAP
 #define PT_WF_BOUNCE_CAP 8192  // bounce grid (blocks) after the first iteration; threads loop over the live list
+#endif
+#ifndef PT_WF_MNT
+#define PT_WF_MNT 0  // non-temporal march result stores
 #endif
 #ifndef PT_WF_STORE_LATE
 #define PT_WF_STORE_LATE 1  // march: a finished job's results are stored after the next job's loads have landed
@@ -947,8 +952,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 have = q < per && pos(q) < count;
                 if (have) start_job(pos(q));
                 if (PT_WF_STORE_LATE) {
+#if PT_WF_MNT
+                    __builtin_nontemporal_store(fbest, v.out.t() + fid);
+                    __builtin_nontemporal_store((int32_t)fwho, v.out.who() + fid);
+#else
                     v.out.t()[fid] = fbest;
                     v.out.who()[fid] = fwho;
+#endif
                 }
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ranks", default="", help="subset of ranks to time (default: all)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a renderer tuning option (pt_renderer_set_option), repeatable")
     a = ap.parse_args()
     import torch
     import __graft_entry__ as ge
@@ -40,6 +42,9 @@ def main():
     text = (ROOT / "scenes" / "cornell_box.json").read_text()
     scene = pt.Scene.from_json(text, seed=1)
     r = pt.HipRenderer(scene, device=0, depth=8)
+    for o in a.option:
+        k, v = o.split("=", 1)
+        r.set_option(k, int(v))
     cam = scene.camera()
     W, H, spp = a.width, a.height, a.spp
     stream = torch.cuda.Stream()

@@ -441,14 +441,18 @@ def main():
         if tr and world == 1 and not multi:
             kind = tr.get("kinds", {}).get(dom)
             if kind:
-                rec["roofline"]["traffic"] = round(kind["traffic"])
+                # the PMC pass's bytes per frame (launches x bytes per launch) spread over this frame's launches
+                # of the kernel: bytes per sample do not depend on the chunking, bytes per launch do
+                frame_bytes = kind["traffic"] * kind.get("launches", dom_n // nfr)
+                per_launch = frame_bytes / max(1, dom_n // nfr)
+                rec["roofline"]["traffic"] = round(per_launch)
                 rec["roofline"]["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % tf.relative_to(ROOT)
-                rec["roofline"]["traffic_gbs"] = round(kind["traffic"] / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
-                # per sample, independent of the chunk size (bytes per launch scale with the paths per chunk)
-                rec["roofline"]["traffic_per_sample"] = round(kind["traffic"] * dom_n / (W * H * spp), 1)
-                if kind.get("launches") not in (None, dom_n):
-                    rec["roofline"]["traffic_note"] = "PMC file launches %s != %d launches per frame here" % (
-                        kind["launches"], dom_n)
+                rec["roofline"]["traffic_gbs"] = round(per_launch / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
+                rec["roofline"]["traffic_per_sample"] = round(frame_bytes / (W * H * spp), 1)
+                if kind.get("launches") not in (None, dom_n // nfr):
+                    rec["roofline"]["traffic_note"] = ("PMC pass: %s launches per frame (two chunk streams); %d here: "
+                                                       "its bytes per frame spread over them" % (kind["launches"],
+                                                                                                 dom_n // nfr))
         if not args.no_parity:
             import oracle
             px = parity_pixels(args)

@@ -217,15 +217,20 @@ def parity_pixels(args):
     return np.unique(np.concatenate([grid, row, col])).astype(np.uint32)
 
 
-def profile_file(name, workload):
-    """A committed PMC result (profiles/rN/<name>) of this workload, newest round first."""
-    for rnd in ("r2", "r1"):
+def profile_file(name, workload, source):
+    """A committed PMC result (profiles/rN/<name>) of this workload, newest round first, and whether it was
+    collected on this build (its source_id == the loaded library's): (path, record, why_not)."""
+    for rnd in ("r3", "r2", "r1"):
         f = ROOT / "profiles" / rnd / name
         if f.exists():
             tr = json.loads(f.read_text())
-            if tr.get("workload") == workload:
-                return f, tr
-    return None, None
+            if tr.get("workload") != workload:
+                continue
+            if tr.get("source_id") != source:
+                return f, None, "%s was collected on build %s, this is %s" % (f.relative_to(ROOT),
+                                                                             tr.get("source_id"), source)
+            return f, tr, None
+    return None, None, "no committed %s for this workload" % name
 
 
 def main():
@@ -284,6 +289,7 @@ def main():
     torch.cuda.synchronize()
 
     k_start, k_end = [], []
+    g_start, g_end = [], []  # the gather + unshard of each step (world > 1), on rank 0's clock
 
     def step():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -298,6 +304,8 @@ def main():
         k_start.append(ev0)
         k_end.append(ev1)
         if world > 1:
+            gv0, gv1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            gv0.record(stream)
             if gloo:
                 shard_h.copy_(shard)  # synchronous D2H on the render stream
                 dist.gather(shard_h, glist, dst=0)
@@ -307,6 +315,9 @@ def main():
                 dist.gather(shard, glist, dst=0)
             if rank == 0:
                 pt.unshard_device(gathered.data_ptr(), W, H, world, frame.data_ptr(), sp, device=local)
+            gv1.record(stream)
+            g_start.append(gv0)
+            g_end.append(gv1)
 
     for _ in range(args.warmup):
         step()
@@ -314,6 +325,8 @@ def main():
     pt.march_guard_drops(r)  # clear
     k_start.clear()
     k_end.clear()
+    g_start.clear()
+    g_end.clear()
     pt.kernel_timing(r, True)  # per-kernel HIP events on the launch stream, timed steps only
     if world > 1:
         dist.barrier()
@@ -328,6 +341,7 @@ def main():
     kt = pt.kernel_timing(r, False)
     guard_drops = pt.march_guard_drops(r)
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
+    gather_ms = sum(a.elapsed_time(b) for a, b in zip(g_start, g_end)) / max(1, len(g_start))
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -335,6 +349,8 @@ def main():
     else:
         kernel_ms_max = kernel_ms
 
+    # parity is checked on the last timed frame (the one behind `value`): copy it out before the roofline leg
+    img = frame.view(-1, 3).cpu().numpy() if rank == 0 else None
     # roofline leg: one frame with every render kernel alone on the device (one chunk stream)
     kt_iso = None
     if not args.no_roofline_leg:
@@ -347,14 +363,10 @@ def main():
         torch.cuda.synchronize()
         kt_iso = pt.kernel_timing(r, False)
         r.set_option("wf_slots", slots)
-        if world > 1:  # the last timed frame is what rank 0 checks: render it again
-            step()
-            torch.cuda.synchronize()
 
     if rank == 0:
         samples_frame = W * H * spp
         value = samples_frame * args.steps / elapsed / 1e6
-        img = frame.view(-1, 3).cpu().numpy()
         sys.path.insert(0, str(ROOT / "oracle"))
 
         # roofline of the dominant kernel (this rank's / the first device's launches)
@@ -369,7 +381,9 @@ def main():
         workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
         # algorithmic FLOPs per sample: from the f64 instruction counters of a committed PMC pass of this
         # workload (scripts/pmc_flops.py) when there is one, else the event counts times FLOP_WEIGHTS
-        ff, fl = profile_file("pmc_flops_c2.json", workload)
+        cfg = args.config or ("c2" if metric_name(args) == METRIC else None)
+        src_id = pt.source_id()
+        ff, fl, f_why = profile_file("pmc_flops_%s.json" % cfg, workload, src_id) if cfg else (None, None, "no config")
         f_kind = dict(f_weights)
         if fl:
             for k, v in fl["kinds"].items():
@@ -418,7 +432,7 @@ def main():
                                           "event weights give %.1f FLOP/sample (%.2fx)"
                                           % (ff.relative_to(ROOT), f_weights["bounce"] + f_weights["march"],
                                              (f_weights["bounce"] + f_weights["march"]) / F) if fl else
-                                          "kernel event counters (pt_count_work) x FLOP_WEIGHTS"),
+                                          "kernel event counters (pt_count_work) x FLOP_WEIGHTS (%s)" % f_why),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},
                          # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
@@ -432,12 +446,32 @@ def main():
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
             "march_guard_drops": guard_drops,
+            "frame_plan": {"chunks_per_frame": kt["reduce"][1] // max(1, args.steps), "chunk_streams": slots,
+                           "note": "the timed frames' sample chunks (one wf_reduce each) on this rank / first device"},
         }
+        per_rank_tiles = [pt.shard_tiles(W, H, k, n_gpus) for k in range(n_gpus)]
+        rec["rank_share"] = {"tiles_total": pt.shard_tiles(W, H, 0, 1), "tiles_per_rank_max": max(per_rank_tiles),
+                             "tiles_per_rank_min": min(per_rank_tiles),
+                             "samples_per_rank_max": max(per_rank_tiles) * 256 * spp,
+                             "deal": "16x16 tiles, logical tile k -> rank k % N, diagonal columns"}
+        if world > 1:
+            rec["gather"] = {"bytes_per_rank": per * 256 * 3 * 8, "bytes_total": world * per * 256 * 3 * 8,
+                             "ms_per_step": round(gather_ms, 3),
+                             "what": ("dist.gather of the compact f64 shards to rank 0 (%s) + pt_unshard_device, "
+                                      "HIP events on rank 0's stream" % ("gloo, through host memory" if gloo
+                                                                         else "RCCL"))}
+        if multi:
+            pairs, enabled = r.peer_access()
+            rec["gather"] = {"bytes_total": args.gpus * pt.shard_tiles(W, H, 0, args.gpus) * 256 * 3 * 8,
+                             "peer_pairs": pairs, "peer_access_enabled": enabled,
+                             "what": "hipMemcpyPeerAsync of each device's shard to the first device, per band"}
         if tuning:
             rec["tuning"] = tuning
         # roofline.traffic: HBM bytes per launch of the same kernel from the committed PMC passes of this
         # workload (scripts/pmc_traffic.py; bench.py cannot read PMC counters itself)
-        tf, tr = profile_file("pmc_traffic_c2.json", workload)
+        tf, tr, t_why = profile_file("pmc_traffic_%s.json" % cfg, workload, src_id) if cfg else (None, None, "no config")
+        if not tr:
+            rec["roofline"]["traffic_source"] = t_why
         if tr and world == 1 and not multi:
             kind = tr.get("kinds", {}).get(dom)
             if kind:
@@ -468,6 +502,10 @@ def main():
                                     % (min(H - 1, H * 757 // 1080), min(W - 1, W * 1142 // 1920), spp,
                                        time.perf_counter() - t) if not args.parity_pixels
                                     else "%d random pixels" % len(px))
+            rec["parity_frame"] = ("the last timed step's frame (the one behind `value`: %d chunks on %d chunk "
+                                   "streams%s), copied out before the roofline leg"
+                                   % (rec["frame_plan"]["chunks_per_frame"], slots,
+                                      ", gathered from %d ranks" % world if world > 1 else ""))
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(text, args)
         print(json.dumps(rec), flush=True)

@@ -66,13 +66,23 @@ typedef struct pt_renderer pt_renderer;
 typedef int (*pt_image_loader)(void *user, const char *filename, uint32_t *width, uint32_t *height,
                                const uint8_t **rgba8);
 
+/* The struct is versioned by struct_size, which the library honours: it reads
+ * no byte at or past opts + struct_size.  A caller sets struct_size =
+ * sizeof(pt_scene_opts) of the header it was compiled against (or uses
+ * PT_SCENE_OPTS_INIT).  struct_size == 0 is a version-1 caller (0.2.0 and
+ * earlier, this field was `reserved`, always 0): its struct is the 16 bytes
+ * {random_spheres, reserved, seed} and load_image / image_user are never
+ * read.  A size between 1 and 15 is rejected (PT_ERR_INVALID); fields a newer
+ * caller appends past sizeof(pt_scene_opts) are ignored. */
 typedef struct {
     uint32_t random_spheres; /* 1 = reference behaviour (default), 0 = JSON shapes only */
-    uint32_t reserved;
+    uint32_t struct_size;    /* sizeof(pt_scene_opts); 0 = version-1 16-byte struct */
     uint64_t seed; /* seed of the add_random_spheres stream and of the NoiseTexture Perlin tables */
-    pt_image_loader load_image; /* NULL: built-in PPM reader */
+    pt_image_loader load_image; /* NULL: built-in PPM reader (read only if struct_size covers it) */
     void *image_user;
 } pt_scene_opts;
+#define PT_SCENE_OPTS_V1_SIZE 16
+#define PT_SCENE_OPTS_INIT {1u, (uint32_t)sizeof(pt_scene_opts), 1u, NULL, NULL}
 
 /* Camera (src/camera/mod.rs:36-46).  fov in radians, as Camera::new takes it. */
 typedef struct {
@@ -137,6 +147,14 @@ int pt_renderer_create(pt_scene *scene, int device, uint32_t depth, pt_renderer 
  * one-device render (the RNG is keyed per (pixel, sample)). */
 int pt_renderer_create_multi(pt_scene *scene, const int *devices, int ngpu, uint32_t depth, pt_renderer **out);
 int pt_renderer_num_devices(const pt_renderer *r);
+/* Peer access of a multi-device renderer.  Create enables it both ways
+ * between devices[0] and every other distinct device that can reach it
+ * (hipDeviceCanAccessPeer, then hipDeviceEnablePeerAccess; "already enabled"
+ * counts as enabled), so the shard copies go device to device over xGMI.  A
+ * pair that cannot be enabled still works: hipMemcpyPeerAsync stages it.
+ * *pairs = distinct (devices[0], devices[k]) pairs, *enabled = those with
+ * peer access on both ways.  A repeated ordinal is no pair. */
+int pt_renderer_peer_access(const pt_renderer *r, int *pairs, int *enabled);
 /* Tuning knobs of the render engines (not part of the reference; defaults are
  * the measured optimum): "engine" (0 auto, 1 megakernel,
  * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
@@ -167,10 +185,11 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking);
  * the encoded rows of every finished band; rgb (may be NULL) the linear ones.
  * Same return values as pt_render_step. */
 int pt_render_step_rgba8(pt_renderer *r, double *rgb, uint8_t *rgba, int blocking);
-/* Renderer::stop_rendering (mod.rs:55): the frame in flight is abandoned — its
- * queued kernels see the renderer's stop flag and skip their work — and the
- * call returns when the device streams are drained.  Bands already copied by
- * render_step stay valid; the rest of the buffer is not written. */
+/* Renderer::stop_rendering (mod.rs:55): the frame in flight is abandoned.  No
+ * further band is queued; the bands already queued (at most two, each about
+ * 1/8 of the frame) still run, and the call returns once the device streams
+ * have drained them.  Bands already copied by render_step stay valid; the
+ * rest of the buffer is not written. */
 int pt_render_stop(pt_renderer *r);
 
 /* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */
@@ -195,7 +214,8 @@ int pt_render_frame_device(pt_renderer *r, const pt_camera *camera, uint32_t wid
 uint32_t pt_shard_tiles(uint32_t width, uint32_t height, uint32_t rank, uint32_t world);
 /* Rebuild the frame from `world` gathered shard buffers laid out back to back,
  * each padded to pt_shard_tiles(w, h, 0, world) tiles, on HIP device `device`
- * (-1 = the calling thread's current device) and its stream hip_stream. */
+ * (-1 = the calling thread's current device) and its stream hip_stream.
+ * (ABI version 3 added the leading `device`; see PT_ABI_VERSION.) */
 int pt_unshard_device(int device, const double *d_gathered, uint32_t width, uint32_t height, uint32_t world,
                       double *d_frame, void *hip_stream);
 
@@ -239,7 +259,8 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
  * iterations (each >= 1 reference step) is one the reference would not finish
  * either — e.g. a step below the rounding of t, where t + step == t and
  * ray_marching.rs:37-51 loops forever; it is taken as a miss (the ray goes on
- * to the shape's neighbours) and counted here.  Waits for the devices. */
+ * to the shape's neighbours) and counted here.  Waits for the devices.
+ * PT_ERR_STATE while a render_start frame is in flight. */
 int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
 
 /* Per-kernel launch timing of the render path (bench / roofline): returns
@@ -247,7 +268,8 @@ int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
  * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
  * reduce, [4] megakernel — into ms[nkinds] / launches[nkinds] (either may be
  * NULL), then turns recording on (enable = 1) or off.  Events are recorded on
- * the stream each kernel is launched on. */
+ * the stream each kernel is launched on.  PT_ERR_STATE while a render_start
+ * frame is in flight (its band feeder records into the same timer). */
 #define PT_KERNEL_KINDS 5
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
 
@@ -257,7 +279,8 @@ int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches,
  * phase (4), then the bounce kernel's cycles per section (list load, state
  * loads, shade, unwind, trace, march pre-check, stores; each section ended by
  * a full s_waitcnt, so the waits it causes are charged to it) — and turns the
- * instrumented build on (enable = 1) or off. */
+ * instrumented build on (enable = 1) or off.  PT_ERR_STATE while a
+ * render_start frame is in flight. */
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
 
 /* Diagnostic: render the whole frame (depth <= 8) with a timing build of the
@@ -286,6 +309,25 @@ uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample);
 
 const char *pt_last_error(void);
 const char *pt_version(void);
+
+/* ---- ABI self-description ----------------------------------------------- */
+/* PT_ABI_VERSION changes whenever an entry point's signature or a struct's
+ * layout changes (3: pt_scene_opts.struct_size, pt_unshard_device's leading
+ * `device`, pt_abi_layout).  A binding compares it with the value it was
+ * written for before calling anything else. */
+#define PT_ABI_VERSION 3
+uint32_t pt_abi_version(void);
+/* Layout of a boundary struct as the library was compiled: out[0] = sizeof,
+ * out[1 + k] = offsetof of the k-th field in declaration order.  Writes
+ * min(n, fields + 1) values and returns fields + 1, or PT_ERR_INVALID for an
+ * unknown `which`.  A binding (ctypes, Rust #[repr(C)]) checks its own
+ * declarations against it. */
+#define PT_ABI_SCENE_OPTS 0    /* 5 fields */
+#define PT_ABI_CAMERA 1        /* 6 fields: position, direction, up, right, fov, focal_length */
+#define PT_ABI_SHAPE_INFO 2    /* 20 fields, as declared */
+#define PT_ABI_MATERIAL_INFO 3 /* 6 fields */
+#define PT_ABI_HIT 4           /* 7 fields */
+int pt_abi_layout(int which, uint32_t *out, size_t n);
 
 #ifdef __cplusplus
 }

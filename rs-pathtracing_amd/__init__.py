@@ -45,8 +45,9 @@ EXPORTS = [
     "pt_render_device", "pt_render_frame_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit",
     "pt_ray_color", "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_march_guard_drops", "pt_wave_diag",
     "pt_kernel_timing", "pt_encode_rgba8", "pt_encode_rgba8_device", "pt_write_png", "pt_write_ppm",
-    "pt_sample_key", "pt_last_error", "pt_version",
+    "pt_sample_key", "pt_last_error", "pt_version", "pt_abi_version", "pt_abi_layout", "pt_renderer_peer_access",
 ]
+ABI_VERSION = 3  # PT_ABI_VERSION this binding is written for
 
 
 class PtError(RuntimeError):
@@ -63,7 +64,7 @@ ImageLoader = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32)
 
 
 class SceneOpts(C.Structure):
-    _fields_ = [("random_spheres", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_uint64),
+    _fields_ = [("random_spheres", C.c_uint32), ("struct_size", C.c_uint32), ("seed", C.c_uint64),
                 ("load_image", ImageLoader), ("image_user", C.c_void_p)]
 
 
@@ -162,6 +163,9 @@ def lib():
         "pt_sample_key": (u64, [u64, u64, u64]),
         "pt_last_error": (C.c_char_p, []),
         "pt_version": (C.c_char_p, []),
+        "pt_abi_version": (u32, []),
+        "pt_abi_layout": (C.c_int, [C.c_int, C.POINTER(u32), sz]),
+        "pt_renderer_peer_access": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("PT_AMD_LIB") and not hasattr(L, name):
@@ -169,6 +173,9 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if not os.environ.get("PT_AMD_LIB") and L.pt_abi_version() != ABI_VERSION:
+        raise ImportError("%s has ABI version %d; this binding is written for %d (rebuild the library)"
+                          % (LIB_PATH, L.pt_abi_version(), ABI_VERSION))
     _lib = L
     return L
 
@@ -229,7 +236,7 @@ class Scene:
         (src/world/texture.rs:119-130).  Names not in it are read by the
         library's built-in binary-PPM reader."""
         raw = data.encode("utf-8") if isinstance(data, str) else bytes(data)
-        opts = SceneOpts(1 if random_spheres else 0, 0, seed)
+        opts = SceneOpts(1 if random_spheres else 0, C.sizeof(SceneOpts), seed)
         keep = []
         if images:
             def load(_user, name, w, h, px):
@@ -316,6 +323,12 @@ class HipRenderer(Renderer):
     @property
     def num_devices(self) -> int:
         return _check(lib().pt_renderer_num_devices(self._h))
+
+    def peer_access(self) -> tuple:
+        """(distinct device pairs with devices[0], pairs with peer access enabled both ways)."""
+        p, e = C.c_int(), C.c_int()
+        _check(lib().pt_renderer_peer_access(self._h, C.byref(p), C.byref(e)))
+        return p.value, e.value
 
     def set_option(self, name: str, value: int):
         """A tuning knob (pt_renderer_set_option): "engine" 0 auto / 1 megakernel / 2 wavefront, "wf_slots", ..."""
@@ -579,3 +592,20 @@ def sample_key(seed: int, pixel: int, sample: int) -> int:
 
 def version() -> str:
     return lib().pt_version().decode()
+
+
+def source_id() -> str:
+    """The loaded build's source hash (pt_version's "src ..." field, rs-pathtracing_amd/Makefile)."""
+    v = version()
+    return v.split("src ", 1)[1].rstrip(")") if "src " in v else "unknown"
+
+
+# pt_abi_layout struct ids and the ctypes mirror of each
+ABI_STRUCTS = {0: SceneOpts, 1: CameraStruct, 2: ShapeInfo, 3: MaterialInfo, 4: HitStruct}
+
+
+def abi_layout(which: int) -> list:
+    """[sizeof, offsetof(field 0), ...] of a boundary struct as the library was compiled (pt_abi_layout)."""
+    out = (C.c_uint32 * 64)()
+    n = _check(lib().pt_abi_layout(int(which), out, 64))
+    return list(out[:n])

@@ -6,9 +6,11 @@
 // frame is still on the GPU (src/renderer/step_by_step.rs:101-121).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstddef>
 #include <cstring>
 #include <new>
 #include <string>
@@ -88,6 +90,7 @@ struct pt_renderer {
     size_t rgba_cap = 0;
     double *d_gather = nullptr;  // multi-device: world shards back to back, on gpus[0]
     size_t gather_cap = 0;
+    int peer_pairs = 0, peer_enabled = 0;  // distinct (gpus[0], gpus[k]) device pairs; with peer access both ways
     // A progressive frame is a list of bands of tile rows.  A feeder thread
     // queues them on the device(s), keeping two bands ahead of the GPU (one
     // running, one queued), so the device never idles between bands and
@@ -114,20 +117,72 @@ extern "C" {
 
 const char *pt_last_error(void) { return g_err.c_str(); }
 __attribute__((visibility("hidden"))) void pt_set_last_error(const char *msg) { g_err = msg ? msg : ""; }  // for pt_image.cpp
-const char *pt_version(void) { return "rs-pathtracing-amd 0.2.0 (gfx950, f64 megakernel + wavefront march engine)"; }
+#ifndef PT_SRC_SHA
+#define PT_SRC_SHA "unknown"
+#endif
+const char *pt_version(void) {
+    return "rs-pathtracing-amd 0.3.0 (gfx950, f64 megakernel + wavefront march engine; src " PT_SRC_SHA ")";
+}
+uint32_t pt_abi_version(void) { return PT_ABI_VERSION; }
+
+int pt_abi_layout(int which, uint32_t *out, size_t n) {
+    std::vector<size_t> v;
+#define PT_F(T, f) v.push_back(offsetof(T, f))
+    switch (which) {
+    case PT_ABI_SCENE_OPTS:
+        v.push_back(sizeof(pt_scene_opts));
+        PT_F(pt_scene_opts, random_spheres), PT_F(pt_scene_opts, struct_size), PT_F(pt_scene_opts, seed);
+        PT_F(pt_scene_opts, load_image), PT_F(pt_scene_opts, image_user);
+        break;
+    case PT_ABI_CAMERA:
+        v.push_back(sizeof(pt_camera));
+        PT_F(pt_camera, position), PT_F(pt_camera, direction), PT_F(pt_camera, up), PT_F(pt_camera, right);
+        PT_F(pt_camera, fov), PT_F(pt_camera, focal_length);
+        break;
+    case PT_ABI_SHAPE_INFO:
+        v.push_back(sizeof(pt_shape_info));
+        PT_F(pt_shape_info, type), PT_F(pt_shape_info, material), PT_F(pt_shape_info, inverse_normal);
+        PT_F(pt_shape_info, depth), PT_F(pt_shape_info, func), PT_F(pt_shape_info, pad0);
+        PT_F(pt_shape_info, direct), PT_F(pt_shape_info, inverse);
+        PT_F(pt_shape_info, x0), PT_F(pt_shape_info, y0), PT_F(pt_shape_info, x1), PT_F(pt_shape_info, y1);
+        PT_F(pt_shape_info, step), PT_F(pt_shape_info, a), PT_F(pt_shape_info, b), PT_F(pt_shape_info, c);
+        PT_F(pt_shape_info, d), PT_F(pt_shape_info, sphere_radius), PT_F(pt_shape_info, radius);
+        PT_F(pt_shape_info, tube_radius);
+        break;
+    case PT_ABI_MATERIAL_INFO:
+        v.push_back(sizeof(pt_material_info));
+        PT_F(pt_material_info, type), PT_F(pt_material_info, texture), PT_F(pt_material_info, albedo);
+        PT_F(pt_material_info, fuzz), PT_F(pt_material_info, ior), PT_F(pt_material_info, emit);
+        break;
+    case PT_ABI_HIT:
+        v.push_back(sizeof(pt_hit));
+        PT_F(pt_hit, t), PT_F(pt_hit, point), PT_F(pt_hit, normal), PT_F(pt_hit, front_face);
+        PT_F(pt_hit, shape), PT_F(pt_hit, material), PT_F(pt_hit, pad0);
+        break;
+    default:
+        return fail(PT_ERR_INVALID, "pt_abi_layout: unknown struct " + std::to_string(which));
+    }
+#undef PT_F
+    if (n && !out) return fail(PT_ERR_INVALID, "null argument");
+    for (size_t k = 0; k < n && k < v.size(); k++) out[k] = (uint32_t)v[k];
+    return (int)v.size();
+}
 
 uint64_t pt_sample_key(uint64_t seed, uint64_t pixel, uint64_t sample) { return sample_key(seed, pixel, sample); }
 
 int pt_scene_create_from_json(const char *json, size_t len, const pt_scene_opts *opts, pt_scene **out) {
     if (!json || !out) return fail(PT_ERR_INVALID, "null argument");
     *out = nullptr;
+    // struct_size versions the options (header): no byte at or past
+    // opts + struct_size is read; 0 is a version-1 caller's 16-byte struct
+    const size_t osz = !opts ? 0 : (opts->struct_size ? opts->struct_size : (size_t)PT_SCENE_OPTS_V1_SIZE);
+    if (opts && osz < PT_SCENE_OPTS_V1_SIZE)
+        return fail(PT_ERR_INVALID, "pt_scene_opts.struct_size " + std::to_string(osz) + " is below the 16-byte version-1 struct");
     bool rs = opts ? opts->random_spheres != 0 : true;
     uint64_t seed = opts ? opts->seed : 1;
     ImageSource img;
-    if (opts) {
-        img.load = opts->load_image;
-        img.user = opts->image_user;
-    }
+    if (opts && osz >= offsetof(pt_scene_opts, load_image) + sizeof(opts->load_image)) img.load = opts->load_image;
+    if (opts && osz >= offsetof(pt_scene_opts, image_user) + sizeof(opts->image_user)) img.user = opts->image_user;
     try {
         pt_scene *s = new pt_scene;
         try {
@@ -417,6 +472,38 @@ void join_feeder(pt_renderer *r) {
     if (r->feeder.joinable()) r->feeder.join();
 }
 
+// Peer access between gpus[0] (which holds the frame) and every other distinct
+// device, both ways, so hipMemcpyPeerAsync of a shard goes device to device
+// over xGMI instead of staging through the host.  A pair the hardware cannot
+// reach stays on the staged copy (still correct).
+int enable_peers(pt_renderer *r) {
+    const int d0 = r->gpus[0].device;
+    std::vector<int> seen;
+    for (size_t k = 1; k < r->gpus.size(); k++) {
+        const int dk = r->gpus[k].device;
+        if (dk == d0 || std::find(seen.begin(), seen.end(), dk) != seen.end()) continue;
+        seen.push_back(dk);
+        r->peer_pairs++;
+        int a = 0, b = 0;
+        HIP_TRY(hipDeviceCanAccessPeer(&a, dk, d0));
+        HIP_TRY(hipDeviceCanAccessPeer(&b, d0, dk));
+        if (!a || !b) continue;
+        bool ok = true;
+        for (int way = 0; way < 2; way++) {
+            HIP_TRY(hipSetDevice(way == 0 ? dk : d0));
+            const hipError_t e = hipDeviceEnablePeerAccess(way == 0 ? d0 : dk, 0);
+            if (e == hipErrorPeerAccessAlreadyEnabled) {
+                (void)hipGetLastError();  // clear the sticky "already enabled"
+            } else if (e != hipSuccess) {
+                return hip_fail(e, "hipDeviceEnablePeerAccess");
+            }
+            ok = ok && (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled);
+        }
+        if (ok) r->peer_enabled++;
+    }
+    return PT_OK;
+}
+
 int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t depth, pt_renderer **out) {
     *out = nullptr;
     if (depth > 64) return fail(PT_ERR_UNSUPPORTED, "depth > 64 is not supported on the GPU path");
@@ -447,6 +534,10 @@ int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t d
     } catch (const std::bad_alloc &) {
         pt_renderer_destroy(r);
         return fail(PT_ERR_INVALID, "out of memory");
+    }
+    if (int rc = enable_peers(r)) {
+        pt_renderer_destroy(r);
+        return rc;
     }
     (void)hipSetDevice(devices[0]);
     *out = r;
@@ -509,6 +600,13 @@ const char *pt_option_name(int index) {
     int n = 0;
     while (TUNING_NAMES[n]) n++;
     return index >= 0 && index < n ? TUNING_NAMES[index] : nullptr;
+}
+
+int pt_renderer_peer_access(const pt_renderer *r, int *pairs, int *enabled) {
+    if (!r) return fail(PT_ERR_INVALID, "null renderer");
+    if (pairs) *pairs = r->peer_pairs;
+    if (enabled) *enabled = r->peer_enabled;
+    return PT_OK;
 }
 
 int pt_renderer_num_devices(const pt_renderer *r) { return r ? (int)r->gpus.size() : fail(PT_ERR_INVALID, "null renderer"); }
@@ -800,6 +898,7 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
 
 int pt_march_guard_drops(pt_renderer *r, uint64_t *count) {
     if (!r || !count) return fail(PT_ERR_INVALID, "null argument");
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
     uint64_t total = 0;
     for (auto &g : r->gpus) {
         HIP_TRY(hipSetDevice(g.device));
@@ -815,6 +914,8 @@ int pt_march_guard_drops(pt_renderer *r, uint64_t *count) {
 
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
+    // the band feeder pushes into the timer and may queue timed launches
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
     HIP_TRY(hipSetDevice(r->device()));
     double m[K_KINDS];
     uint32_t l[K_KINDS];
@@ -833,6 +934,8 @@ int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches,
 
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
+    // the band feeder may queue launches that use the diag buffer
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
     HIP_TRY(hipSetDevice(r->device()));
     HIP_TRY(hipStreamSynchronize(r->stream()));
     if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 48 ? n : 48) * 8, hipMemcpyDeviceToHost));

@@ -23,6 +23,15 @@ import csv
 import glob
 import json
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def source_id():
+    """The build the counters were collected on (bench.py uses the file only for that build)."""
+    import __graft_entry__
+    return __graft_entry__.load_package().source_id()
 
 d, frames, samples, out, workload = sys.argv[1], int(sys.argv[2]), float(sys.argv[3]), sys.argv[4], sys.argv[5]
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -32,7 +41,7 @@ for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         kind = "bounce" if "wf_bounce" in name else "march" if "wf_march" in name else None
         if kind:
             acc[kind][row["Counter_Name"]] += float(row["Counter_Value"])
-res = {"workload": workload, "frames": frames, "samples_per_frame": samples,
+res = {"workload": workload, "source_id": source_id(), "frames": frames, "samples_per_frame": samples,
        "source": "rocprofv3 --pmc SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU",
        "kinds": {}}
 for kind, c in acc.items():

@@ -11,6 +11,15 @@ import csv
 import glob
 import json
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def source_id():
+    """The build the counters were collected on (bench.py uses the file only for that build)."""
+    import __graft_entry__
+    return __graft_entry__.load_package().source_id()
 
 KINDS = {"pt::wf_bounce<": "bounce", "pt::wf_march<": "march", "pt::render_tiles": "megakernel"}
 
@@ -40,7 +49,7 @@ def main():
     fetch_dir, write_dir, out, workload = sys.argv[1:5]
     fetch, nf = collect(fetch_dir, "FETCH_SIZE")
     write, nw = collect(write_dir, "WRITE_SIZE")
-    rec = {"workload": workload, "unit": "bytes per launch",
+    rec = {"workload": workload, "source_id": source_id(), "unit": "bytes per launch",
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "kinds": {}}
     for k in sorted(set(fetch) & set(write)):

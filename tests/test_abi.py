@@ -72,3 +72,64 @@ def test_renderer_without_gpu_fails_loudly(pt, cornell_text):
     with pytest.raises(pt.PtError) as e:
         pt.HipRenderer(sc, depth=8)
     assert e.value.code == pt.PT_ERR_HIP
+
+
+# ---- struct layout across the boundary (a 16-byte Rust struct was read as 32) ----
+
+NATIVE = ROOT / "tests" / "native"
+
+
+def abi_check_bin():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(NATIVE), "_build/abi_check"], check=True)
+    return str(NATIVE / "_build" / "abi_check")
+
+
+def test_abi_version(pt):
+    assert pt.lib().pt_abi_version() == pt.ABI_VERSION == 3
+
+
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4])
+def test_abi_layout_matches_ctypes(pt, which):
+    """pt_abi_layout (the library's own sizeof / offsetof) == the ctypes mirror."""
+    S = pt.ABI_STRUCTS[which]
+    assert pt.abi_layout(which) == [C.sizeof(S)] + [getattr(S, f[0]).offset for f in S._fields_]
+
+
+def test_abi_layout_unknown_struct(pt):
+    with pytest.raises(pt.PtError) as e:
+        pt.abi_layout(99)
+    assert e.value.code == pt.PT_ERR_INVALID
+
+
+def test_plain_c_caller_layout():
+    """A gcc-compiled C program, header only: every struct's sizeof / offsetof
+    as C lays it out equals the library's."""
+    import subprocess
+    out = subprocess.run([abi_check_bin(), "layout"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.count("match") == 5
+
+
+def test_version1_opts_are_not_read_past():
+    """A 16-byte version-1 pt_scene_opts placed against an unreadable page: the
+    scene (with an ImageTexture, whose loader field a version-1 struct does not
+    have) loads without touching the page; struct_size 8 is refused."""
+    import subprocess
+    out = subprocess.run([abi_check_bin(), "legacy", "scenes/textured.json"], capture_output=True, text=True,
+                         cwd=str(ROOT))
+    assert out.returncode == 0, (out.returncode, out.stderr)
+    assert "struct_size 8 refused" in out.stdout
+
+
+def test_opts_struct_size_from_python(pt, cornell_text):
+    raw = cornell_text.encode()
+    L = pt.lib()
+    for size, ok in [(0, True), (16, True), (24, True), (32, True), (64, True), (8, False), (15, False)]:
+        o = pt.SceneOpts(0, size, 3)
+        h = C.c_void_p()
+        rc = L.pt_scene_create_from_json(raw, len(raw), C.byref(o), C.byref(h))
+        assert (rc == 0) == ok, (size, rc)
+        if rc == 0:
+            assert L.pt_scene_num_shapes(h) == 9  # random_spheres = 0
+            L.pt_scene_destroy(h)

@@ -31,7 +31,7 @@ def test_ranks_gather_unshard_parity(world):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            str(ROOT / "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
            "--scene", "cornell_box.json", "--width", "320", "--height", "180", "--spp", "4",
-           "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-roofline-leg"]
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -42,3 +42,6 @@ def test_ranks_gather_unshard_parity(world):
     assert "gloo gather" in rec["config"]["parallelism"]
     assert rec["rms_pixels"] >= 700
     assert rec["exact_pixels_frac"] == 1.0 and rec["rms_vs_oracle"] == 0.0
+    # the frame checked is the last timed step's, gathered from every rank (the roofline leg ran after it)
+    assert "gathered from %d ranks" % world in rec["parity_frame"]
+    assert rec["gather"]["bytes_per_rank"] == rec["rank_share"]["tiles_per_rank_max"] * 256 * 3 * 8

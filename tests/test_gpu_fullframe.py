@@ -37,6 +37,74 @@ def test_c2_full_frame_every_pixel(pt, cornell_text):
     assert len(bad) == 0, "%d of %d pixels differ, first %s" % (len(bad), w * h, bad[:10])
 
 
+def _every_pixel(img, ref):
+    rms = np.sqrt(np.mean((img - ref) ** 2, axis=0))
+    assert np.all(rms <= 1e-4), rms
+    bad = np.nonzero(np.any(img != ref, axis=1))[0]
+    assert len(bad) == 0, "%d of %d pixels differ, first %s" % (len(bad), len(img), bad[:10])
+
+
+def test_c2_multichunk_two_streams_every_pixel(pt, cornell_text):
+    """The timed frame's structure at the headline size: several sample chunks
+    on two chunk streams, per-pixel sums chained across the streams in chunk
+    order (pt_wave.hip render_wave_nw) — here 4 chunks of 2 spp (wf_paths =
+    2^22) in two rounds of the 2 streams — every pixel against the oracle
+    (src/renderer/mod.rs:151-155: the in-order per-pixel sum)."""
+    import torch
+    w, h, spp, depth, seed = 1920, 1080, 8, 8, 1
+    ps = pt.Scene.from_json(cornell_text, seed=1)
+    r = pt.HipRenderer(ps, depth=depth)
+    r.set_option("wf_paths", 1 << 22)
+    assert r.get_option("wf_slots") == 2
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    pt.kernel_timing(r, True)
+    r.render_device(ps.camera(), w, h, spp, seed, 0, 1, frame.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    kt = pt.kernel_timing(r, False)
+    assert kt["reduce"][1] == 4  # four chunks, one per-pixel reduce each
+    img = frame.view(-1, 3).cpu().numpy()
+    ref = O.Scene(cornell_text, seed=1).use_bvh(True, 7).render(w, h, spp, depth, seed, threads=host_threads())
+    _every_pixel(img, ref)
+
+
+def test_c3_full_frame_every_pixel(pt, cornell_text):
+    """C3's 3840x2160 frame (BASELINE configs[2]) at 2 spp, every pixel."""
+    import torch
+    w, h, spp, depth, seed = 3840, 2160, 2, 8, 3
+    ps = pt.Scene.from_json(cornell_text, seed=1)
+    r = pt.HipRenderer(ps, depth=depth)
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    r.render_device(ps.camera(), w, h, spp, seed, 0, 1, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    img = frame.view(-1, 3).cpu().numpy()
+    del frame
+    ref = O.Scene(cornell_text, seed=1).use_bvh(True, 7).render(w, h, spp, depth, seed, threads=host_threads())
+    _every_pixel(img, ref)
+
+
+def test_c5_full_frame_every_pixel(pt):
+    """C5's synthetic 100k-sphere scene (BASELINE configs[4]) at 1920x1080, 2 spp,
+    every pixel against the oracle's reference BvhNode traversal
+    (src/world/shapes/mod.rs:620-729)."""
+    import json
+    import sys
+    from pathlib import Path
+    import torch
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    text = json.dumps(make_scenes.synthetic(100000))
+    w, h, spp, depth, seed = 1920, 1080, 2, 8, 2
+    ps = pt.Scene.from_json(text, seed=1)
+    r = pt.HipRenderer(ps, depth=depth)
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    r.render_device(ps.camera(), w, h, spp, seed, 0, 1, frame.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    img = frame.view(-1, 3).cpu().numpy()
+    ref = O.Scene(text, seed=1).use_bvh(True, 7).render(w, h, spp, depth, seed, threads=host_threads())
+    _every_pixel(img, ref)
+
+
 def _compare_hits(got, osc, rays):
     bad = []
     for i, ray in enumerate(rays):

@@ -251,3 +251,52 @@ def test_tuning_options(pt, cornell):
         r.set_option("wf_slots", 1)  # not while a frame is in flight
     r.stop_rendering()
     assert np.array_equal(base, osc.render(64, 40, 3, 8, 4, threads=host_threads()))
+
+
+def test_diagnostics_refused_while_a_frame_is_in_flight(pt, cornell):
+    """kernel_timing / wave_diag / march_guard_drops share state with the band
+    feeder of a non-blocking frame: PT_ERR_STATE until it ends."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h = 1920, 1080
+    buf = np.zeros((w * h, 3))
+    r.start_rendering(cam, pt.ImageParams(w, h), 8, seed=1)
+    for call in (lambda: pt.kernel_timing(r, True), lambda: pt.wave_diag(r, True),
+                 lambda: pt.march_guard_drops(r)):
+        with pytest.raises(pt.PtError) as e:
+            call()
+        assert e.value.code == pt.PT_ERR_STATE
+    while not r.render_step(buf):
+        pass
+    pt.kernel_timing(r, False)  # allowed again once the frame is done
+    assert pt.march_guard_drops(r) == 0
+    sampled_rows_check(osc, buf, w, h, 8, np.arange(h), n=512, seed=3)
+
+
+def test_peer_access_state(pt, cornell):
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8, devices=[0, 0, 0])
+    assert r.peer_access() == (0, 0)  # a repeated ordinal is no device pair
+    assert pt.HipRenderer(ps, depth=8).peer_access() == (0, 0)
+
+
+def test_plain_c_caller_renders_through_the_abi(pt, cornell_text):
+    """tests/native/abi_check.c (gcc, header only): Scene::from_json ->
+    renderer -> start_rendering -> blocking render_step; its frame equals the
+    oracle's bit for bit."""
+    import subprocess
+    import tempfile
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    exe = root / "tests" / "native" / "_build" / "abi_check"
+    assert exe.exists(), "build it on the CPU first: make -C tests/native"
+    w, h, spp = 96, 54, 2
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "frame.f64"
+        p = subprocess.run([str(exe), "render", "scenes/cornell_box.json", str(w), str(h), str(spp), "8", "5",
+                            str(out)], capture_output=True, text=True, cwd=str(root), timeout=100)
+        assert p.returncode == 0, p.stderr
+        img = np.fromfile(out, dtype=np.float64).reshape(-1, 3)
+    ref = O.Scene(cornell_text, seed=1).render(w, h, spp, 8, 5, threads=host_threads())
+    assert np.array_equal(img, ref)

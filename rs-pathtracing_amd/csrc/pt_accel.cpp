@@ -73,7 +73,7 @@ namespace {
 struct Builder {
     const std::vector<DBox> &boxes;
     Accel &out;
-    int leaf_max = 1;  // shapes per leaf (PT_BVH_LEAF; C5 measured 677 / 609 / 534 M samples/s at 1 / 2 / 4)
+    int leaf_max = 1;  // shapes per leaf (Tuning::bvh_leaf; C5 measured 677 / 609 / 534 M samples/s at 1 / 2 / 4)
     // the tree in build order: node box (DNode with first/count for leaves),
     // split axis and children (-1 for a leaf)
     struct TNode {
@@ -140,7 +140,7 @@ struct Builder {
 
 }  // namespace
 
-Accel build_accel(const Scene &sc, int json_shapes) {
+Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
     Accel a;
     a.boxes.reserve(sc.shapes.size());
     for (auto &s : sc.shapes) a.boxes.push_back(shape_box(s));
@@ -178,7 +178,7 @@ Accel build_accel(const Scene &sc, int json_shapes) {
     }
     if (!rest.empty()) {
         Builder b{a.boxes, a};
-        if (const char *e = getenv("PT_BVH_LEAF")) b.leaf_max = std::max(1, std::min(16, atoi(e)));
+        b.leaf_max = std::max(1, std::min(16, leaf_max));
         const int root = b.emit(rest, 0, rest.size());
         a.nodes.reserve(b.tree.size() * BVH_OCTANTS);
         for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());

@@ -41,7 +41,8 @@ struct Accel {
 
 constexpr int LIN_MAX = 32;  // JSON shape count up to which the JSON shapes form `lin`
 
-Accel build_accel(const Scene &sc, int json_shapes);
+// leaf_max: shapes per BVH leaf (the renderer option "bvh_leaf")
+Accel build_accel(const Scene &sc, int json_shapes, int leaf_max = 1);
 // conservative world AABB of one shape (reference get_bounding_box + padding)
 DBox shape_box(const HostShape &s);
 

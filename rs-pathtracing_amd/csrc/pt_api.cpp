@@ -285,6 +285,39 @@ void free_share(GpuShare &g) {
     g.stream = nullptr;
 }
 
+// The acceleration structure on one device (replacing any previous one):
+// octant-threaded BVH nodes, leaf shape ids, the wave-uniform and marched
+// lists and the padded boxes.
+int upload_accel(GpuShare &g, const Accel &acc) {
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    DeviceScene &d = g.ds;
+    void *old[] = {d.nodes, d.leaf, d.lin, d.march, d.boxes};
+    for (void *p : old)
+        if (p) HIP_TRY(hipFree(p));
+    d.nodes = nullptr;
+    d.leaf = d.lin = d.march = nullptr;
+    d.boxes = nullptr;
+    hipError_t err = hipSuccess;
+    auto upload = [&err](auto **dst, const auto &vec) {
+        using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+        size_t n = vec.empty() ? 1 : vec.size();
+        if (err == hipSuccess) err = hipMalloc((void **)dst, n * sizeof(T));
+        if (err == hipSuccess && !vec.empty())
+            err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice);
+    };
+    upload(&d.nodes, acc.cnodes);
+    upload(&d.leaf, acc.leaf);
+    upload(&d.lin, acc.lin);
+    upload(&d.march, acc.march);
+    upload(&d.boxes, acc.boxes);
+    if (err != hipSuccess) return hip_fail(err, "uploading the acceleration structure");
+    d.nnodes = acc.nodes_per_octant();  // nodes per octant layout
+    d.nlin = (int)acc.lin.size();
+    d.nmarch = (int)acc.march.size();
+    return PT_OK;
+}
+
 // Uploads the realized scene to one device and creates its stream and stop flag.
 int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const std::vector<DShape> &hs,
                const std::vector<DMaterial> &hm) {
@@ -300,11 +333,6 @@ int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const 
     };
     upload(&g.ds.shapes, hs);
     upload(&g.ds.mats, hm);
-    upload(&g.ds.nodes, acc.cnodes);
-    upload(&g.ds.leaf, acc.leaf);
-    upload(&g.ds.lin, acc.lin);
-    upload(&g.ds.march, acc.march);
-    upload(&g.ds.boxes, acc.boxes);
     if (!S.textures.empty()) {
         upload(&g.ds.tex, S.textures);
         upload(&g.ds.perlin, S.perlins);
@@ -315,13 +343,11 @@ int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const 
     if (err == hipSuccess) err = hipMalloc((void **)&g.ds.guard, sizeof(unsigned long long));
     if (err == hipSuccess) err = hipMemset(g.ds.guard, 0, sizeof(unsigned long long));
     if (err != hipSuccess) return hip_fail(err, "uploading the scene");
+    if (int rc = upload_accel(g, acc)) return rc;
     g.ws.tune = tuning_from_env();
     g.ds.diag = g.ws.tune.diag;
     g.ds.nshapes = (int)hs.size();
     g.ds.nmats = (int)hm.size();
-    g.ds.nnodes = acc.nodes_per_octant();  // nodes per octant layout
-    g.ds.nlin = (int)acc.lin.size();
-    g.ds.nmarch = (int)acc.march.size();
     g.ds.ext = S.textures.empty() ? 0 : 1;
     for (const auto &h : S.shapes)
         if (h.type == TORUS) g.ds.ext = 1;
@@ -523,7 +549,7 @@ int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t d
         for (auto &s : scene->s.shapes) hs.push_back(to_device(s));
         for (auto &m : scene->s.materials) hm.push_back(to_device(m));
         if (hm.empty()) hm.push_back(DMaterial{});
-        const Accel acc = build_accel(scene->s, scene->s.json_shapes);
+        const Accel acc = build_accel(scene->s, scene->s.json_shapes, tuning_from_env().bvh_leaf);
         r->gpus.resize(devices.size());
         for (size_t k = 0; k < devices.size(); k++) {
             if (int rc = init_share(r->gpus[k], devices[k], scene->s, acc, hs, hm)) {
@@ -576,6 +602,22 @@ int pt_renderer_create_multi(pt_scene *scene, const int *devices, int ngpu, uint
 int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
     if (!r || !name) return fail(PT_ERR_INVALID, "null argument");
     if (r->started) return fail(PT_ERR_STATE, "options cannot change while a frame is in flight");
+    if (!std::strcmp(name, "bvh_leaf") && value != r->gpus[0].ws.tune.bvh_leaf) {
+        // the BVH is rebuilt with the new leaf size on every device
+        Tuning t = r->gpus[0].ws.tune;
+        if (tuning_set(&t, name, value) != PT_OK)
+            return fail(PT_ERR_INVALID, "bvh_leaf out of range (1..16): " + std::to_string((long long)value));
+        try {
+            const Accel acc = build_accel(r->scene->s, r->scene->s.json_shapes, t.bvh_leaf);
+            for (auto &g : r->gpus) {
+                HIP_TRY(hipSetDevice(g.device));
+                HIP_TRY(hipDeviceSynchronize());
+                if (int rc = upload_accel(g, acc)) return rc;
+            }
+        } catch (const std::exception &e) {
+            return fail(PT_ERR_INVALID, std::string("rebuilding the BVH: ") + e.what());
+        }
+    }
     for (auto &g : r->gpus) {
         Tuning t = g.ws.tune;
         if (tuning_set(&t, name, value) != PT_OK)

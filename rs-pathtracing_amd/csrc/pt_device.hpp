@@ -155,12 +155,6 @@ struct Ray {
     V3 o, d;
 };
 
-#ifndef PT_LAZY_RECT
-#define PT_LAZY_RECT 1
-#endif
-#ifndef PT_LIN_BOX
-#define PT_LIN_BOX 1  // padded-box pre-test for cubes and spheres on the wave-uniform list
-#endif
 // Counts a march dropped by the march guard (pt_march_guard_drops).
 PT_HD void note_guard(unsigned long long *guard) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -178,7 +172,7 @@ template <bool STATS, int FK = march::F_ANY, bool MARCHED = true, bool EXT = fal
 PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t, double *t, Ctr *ct,
                       unsigned long long *guard = nullptr) {
     if (STATS) ct->c[s.type == TORUS ? C_TEST_TORUS : C_TEST_SPHERE + s.type]++;
-    if (PT_LAZY_RECT && s.type == RECTANGLE) {
+    if (s.type == RECTANGLE) {
         // Rectangle: t needs only the object-space z row; x and y are
         // transformed only for a t in range.  Each component is the same
         // expression as in xf_point / xf_vector, so every value is unchanged.
@@ -324,7 +318,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     for (int k = 0; k < sc.nlin; k++) {
         const int i = uniform_load(&sc.lin[k]);
         const DShape s = uniform_shape(&sc.shapes[i]);
-        if (PT_LIN_BOX && (s.type == CUBE || s.type == SPHERE)) {
+        if (s.type == CUBE || s.type == SPHERE) {
             // the padded world box first (12 FLOP with the caller's 1/d):
             // a miss there is a miss of the exact test, which costs a full
             // inverse transform and, for a cube, six divisions
@@ -580,6 +574,9 @@ PT_HD V3 random_in_unit_sphere(Rng &rng, double s11, Ctr *ct = nullptr) {
         double y = rng.uniform(-1.0, s11);
         double z = rng.uniform(-1.0, s11);
         if (x * x + y * y + z * z <= 1.0) return v3(x, y, z);
+#ifdef PT_ABL_ONETRY
+        return v3(x * 0.5, y * 0.5, z * 0.5);  // timing ablation only (not exact): no rejection loop
+#endif
     }
 }
 PT_HD V3 reflect(V3 d, V3 n) {  // algebra/mod.rs:122-125

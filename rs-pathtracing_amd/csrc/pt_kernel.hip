@@ -268,7 +268,7 @@ static dev::Scene dscene(const DeviceScene &s) {
 // ------------------------------------------------------------- tuning
 const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
                                     "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
-                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", nullptr};
+                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "bvh_leaf", nullptr};
 
 static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
     struct F {
@@ -289,6 +289,7 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         {"wf_march_blocks_per_cu", &Tuning::wf_march_blocks_per_cu, 0, 64},
         {"wf_side_priority", &Tuning::wf_side_priority, -1, 1},
         {"wf_pingpong", &Tuning::wf_pingpong, 0, 3},
+        {"bvh_leaf", &Tuning::bvh_leaf, 1, 16},
     };
     *iv = nullptr;
     if (!name) return nullptr;
@@ -339,7 +340,7 @@ Tuning tuning_from_env() {
                {"PT_WF_BOUNCE_WAVES", "wf_bounce_waves"}, {"PT_WF_FUSED", "wf_fused"},
                {"PT_WF_MARCH_SLICE", "wf_march_slice"}, {"PT_WF_TRACE_SLICE", "wf_trace_slice"},
                {"PT_WF_MARCH_BLOCKS_PER_CU", "wf_march_blocks_per_cu"}, {"PT_WF_SIDE_PRIORITY", "wf_side_priority"},
-               {"PT_WF_PINGPONG", "wf_pingpong"}};
+               {"PT_WF_PINGPONG", "wf_pingpong"}, {"PT_BVH_LEAF", "bvh_leaf"}};
     for (const auto &m : map)
         if (const char *e = getenv(m.env)) (void)tuning_set(&t, m.name, atoll(e));  // out of range: default kept
     if (const char *e = getenv("PT_ENGINE")) t.engine = e[0] == 'm' ? 1 : (e[0] == 'w' ? 2 : 0);

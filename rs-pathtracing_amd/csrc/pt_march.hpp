@@ -227,9 +227,6 @@ PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
 // closed-form segment costs ~150 instructions against ~5 per literal add: C2
 // one-stream march 183 -> 172 ms).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
-#ifndef PT_ADV_PEEL
-#define PT_ADV_PEEL 1  // a proven block's four advances start with one straight-line segment each
-#endif
 #ifndef PT_ADV_NZB
 #define PT_ADV_NZB 4  // literal adds per trip in the near-zero zone
 #endif
@@ -351,9 +348,6 @@ PT_HD int64_t steps_in_range(double t, double s, double start, double end, int64
 // exact arithmetic.  heart_poly computes its coefficients; the bound below
 // proves that every f64 evaluation of heart_f at p_1..p_B keeps one sign and
 // stays clear of the 1e-15 stop.
-#ifndef PT_NEWTON
-#define PT_NEWTON 0
-#endif
 struct Poly {
     double g[7];                       // coefficients of g(j)
     double ax, ay, az, cx, cy, cz;     // |p0|, |ch| for the magnitude bound
@@ -483,18 +477,8 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
     return mn > margin;
 }
 
-#ifndef PT_FOLD_LIT
-#define PT_FOLD_LIT 1
-#endif
-#ifndef PT_FOLD_MAX
-#define PT_FOLD_MAX 3  // literal steps an iteration may take when the predicted crossing is that close
-#endif
-#ifndef PT_PREFIX_RES
-#define PT_PREFIX_RES 1.0
-#endif
-#ifndef PT_MAX_LEVELS
-#define PT_MAX_LEVELS 40  // de Casteljau halvings per prefix search
-#endif
+constexpr int FOLD_MAX = 3;     // literal steps an iteration may take when the predicted crossing is that close
+constexpr int MAX_LEVELS = 40;  // de Casteljau halvings per prefix search (capping them: more iterations, slower)
 // Longest provable prefix of a block: the largest integer b <= B such that
 // sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither the
 // approx_equal stop nor a sign change can fire before step b).  One Bernstein
@@ -503,15 +487,10 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 // descends into it.  The margin is the one for the whole block (M and the
 // drift only grow with b), and the halving's own rounding (<= 24 levels of
 // exact-weight averages) stays far inside its 256 eps M part.
-#ifndef PT_TARGET_SPLIT
-#define PT_TARGET_SPLIT 1
-#endif
-#ifndef PT_EM_LEVELS
-#define PT_EM_LEVELS 40  // halvings of a failed early-miss proof (the next proof restarts from a fresh guess)
-#endif
+constexpr int EM_LEVELS = 40;  // halvings of a failed early-miss proof (capped at 8/10/12: slower, round 2 emab)
 template <int FK>
 PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn, double target = 0.0,
-                         int max_levels = PT_MAX_LEVELS) {
+                         int max_levels = MAX_LEVELS) {
     const double margin = poly_margin<FK>(F, P, Bd);
     double a[7];
     double bk = 1.0;
@@ -529,7 +508,7 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
     c[4] = a[0] + a[1] * (2.0 / 3.0) + a[2] * 0.4 + a[3] * 0.2 + a[4] * (1.0 / 15.0);
     c[5] = a[0] + a[1] * (5.0 / 6.0) + a[2] * (2.0 / 3.0) + a[3] * 0.5 + a[4] * (1.0 / 3.0) + a[5] * (1.0 / 6.0);
     c[6] = a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6];
-    if (PT_TARGET_SPLIT && target >= 2.0 && target < Bd) {
+    if (target >= 2.0 && target < Bd) {
         // One split at the step just before the predicted crossing: de
         // Casteljau at lambda >= target / B gives the control points of
         // [0, lambda B], a superset of the steps [1, target]; if they clear
@@ -565,7 +544,7 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
             proven = lo + len;
             break;
         }
-        if (len * Bd < PT_PREFIX_RES) break;  // resolution reached (1 = one step): stop here
+        if (len * Bd < 1.0) break;  // resolution reached (one step): stop here
         // de Casteljau at 1/2 in place: level r overwrites c[0 .. 6-r], so
         // afterwards c[i] is the level-(6-i) point i = the right half's
         // control point i; the left half's are the levels' first points.
@@ -593,8 +572,9 @@ PT_HD double poly_prefix(const FParams &F, const Poly &P, double Bd, double sgn,
 }
 
 // Predicted first crossing (in steps) of sgn*g: the quadratic part's first
-// positive root, polished by Newton steps on the full polynomial; the search
-// starts just before it and the proof decides.
+// positive root (Newton steps on the full polynomial measured worse: misses
+// chase spurious roots of the degree-6 polynomial); the search starts just
+// before it and the proof decides.
 PT_HD double poly_eval(const Poly &P, double j, double *dg) {
     double g = P.g[6], d = 0.0;
 #pragma unroll
@@ -620,49 +600,14 @@ PT_HD double poly_root_guess(const Poly &P, double sgn, double cap) {
     const double rq = disc < 0.0 ? cap : (lo > 0.0 ? lo : (hi > 0.0 ? hi : cap));  // (no real root: no crossing)
     const double rl = S < 0.0 ? L * approx_rcp(-S) : cap;
     double r = fmin(cap, Q == 0.0 ? rl : rq);
-#pragma unroll
-    for (int it = 0; it < PT_NEWTON; it++) {
-        double d, g = poly_eval(P, r, &d);
-        if (!(d != 0.0)) break;
-        double nr = r - g / d;
-        if (!(nr > 0.0)) break;
-        r = fmin(cap, nr);
-    }
     return L <= 0.0 ? 1.0 : r;
 }
 
 // ------------------------------------------------------- the march
-#ifndef PT_SEARCH_DIV
-#define PT_SEARCH_DIV 4
-#endif
-#ifndef PT_SEARCH_START
-#define PT_SEARCH_START 0.999
-#endif
-#ifndef PT_SEARCH_DESCENT
-#define PT_SEARCH_DESCENT 10
-#endif
-#ifndef PT_SEARCH_REFINE
-#define PT_SEARCH_REFINE 10
-#endif
-#ifndef PT_MIN_GUESS
-#define PT_MIN_GUESS 2.0
-#endif
-#ifndef PT_ADV_ROUNDS
-#define PT_ADV_ROUNDS 64  // binade-segment rounds per march_advance call
-#endif
-
-#ifndef PT_EARLY_MISS
-#define PT_EARLY_MISS 1
-#endif
-#ifndef PT_LIT_MAX
-#define PT_LIT_MAX 0.0  // literal-step hint after a prefix stops short (measured slower on the GPU: off)
-#endif
-#ifndef PT_BLOCK_SCALE
-#define PT_BLOCK_SCALE 1.25
-#endif
-#ifndef PT_BLOCK_PAD
-#define PT_BLOCK_PAD 4
-#endif
+constexpr double MIN_GUESS = 2.0;     // a predicted crossing closer than this many steps: literal steps, no proof
+constexpr int ADV_ROUNDS = 64;        // binade-segment rounds per march_advance call
+constexpr double BLOCK_SCALE = 1.25;  // a block is sized BLOCK_SCALE * guess + BLOCK_PAD steps
+constexpr double BLOCK_PAD = 4.0;
 struct MarchStats {
     uint32_t steps, blocks, tries;
     uint32_t guard;  // marches dropped by the MARCH_GUARD (always counted, not only in STATS builds)
@@ -728,7 +673,7 @@ PT_HD bool march_begin(const FParams &F, double step0, int passes, double ox, do
 // One round of a proven block's exact advance: one binade segment for each
 // of t, px, py, pz that still has steps to go; when all are done the block's
 // end point is exact and f is evaluated there.
-template <int FK = F_ANY, int ROUNDS = PT_ADV_ROUNDS>
+template <int FK = F_ANY, int ROUNDS = ADV_ROUNDS>
 PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
     PT_MHOOK(block_begin);
     for (int round = 0; round < ROUNDS; round++) {
@@ -746,7 +691,12 @@ PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
 // One iteration of the march loop: a proven jump, or one literal step (after a
 // failed proof).  M_DONE: the passes ended (the caller applies the final
 // t-in-[min_t, max_t] test); M_MISS: t left [start, end].
-template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
+// DEFER (with INLINE_ADV): a coordinate whose advance does not end with its
+// first binade segment leaves the rest for later: the iteration returns with
+// m.adv set (and the fold's literal steps in m.lit), and a later iteration
+// runs march_advance.  The caller decides when (wf_march batches the lanes of
+// a wave that wait for one); the operations on the job are the same either way.
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY, bool DEFER = false>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
     PT_MPROF(iters);
     int nlit = 1;
@@ -783,24 +733,24 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             const double sgn = m.r > 0.0 ? 1.0 : -1.0;
             const double guess = poly_root_guess(P, sgn, bmax);
             PT_MREG(poly_end);
-            if (guess < PT_MIN_GUESS) {
+            if (guess < MIN_GUESS) {
                 PT_MTRACE(guess, 0, 0, bmax);
-                // the crossing is the next step or two: up to PT_FOLD_MAX
+                // the crossing is the next step or two: up to FOLD_MAX
                 // literal steps in this iteration
-                nlit = guess >= 1.0 ? PT_FOLD_MAX : 1;
+                nlit = guess >= 1.0 ? FOLD_MAX : 1;
                 goto literal;
             }
             // No crossing predicted before the range end: try to prove every
             // step up to (an upper bound on) the one that leaves the range;
             // then nothing can stop this pass first and the march misses.
-            const double ub = PT_EARLY_MISS && guess >= bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIGD;
+            const double ub = guess >= bmax ? steps_exit_ub(m.t, s, m.start, m.end) : BIGD;
             const bool em = ub < BIGD;  // an early-miss proof
-            double B = em ? ub : floor(guess * PT_BLOCK_SCALE) + PT_BLOCK_PAD;
+            double B = em ? ub : floor(guess * BLOCK_SCALE) + BLOCK_PAD;
             if (!em) B = B > bmax ? bmax : (B < 2.0 ? 2.0 : B);
             // the step just before the predicted crossing
             const double target = em ? 0.0 : ceil(guess) - 1.0;
             PT_MREG(prefix_begin);
-            double good = poly_prefix<FK>(m.F, P, B, sgn, target, em ? PT_EM_LEVELS : PT_MAX_LEVELS);
+            double good = poly_prefix<FK>(m.F, P, B, sgn, target, em ? EM_LEVELS : MAX_LEVELS);
             PT_MREG(prefix_end);
             PT_MTRACE(guess, B, good, bmax);
             if (em && good >= ub) return M_MISS;
@@ -812,13 +762,11 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                 m.na[0] = m.na[1] = m.na[2] = m.na[3] = good;
                 m.lim -= good;
                 m.adv = 1;
-                if (PT_LIT_MAX > 0.0 && good < B) m.lit = (int)fmin(PT_LIT_MAX, fmax(1.0, ceil(guess - good)));
                 if (STATS) st->blocks++;
                 if (INLINE_ADV) {
                     // one loop per coordinate: a lane pays only for the binade
                     // segments each coordinate actually crosses
                     PT_MREG(adv_begin);
-#if PT_ADV_PEEL
                     // every coordinate's first segment side by side (four
                     // independent chains), then the rest for those that cross
                     // binade edges
@@ -827,25 +775,29 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     seg_step(m.px, cx, n1);
                     seg_step(m.py, cy, n2);
                     seg_step(m.pz, cz, n3);
+                    if (DEFER && (n0 > 0.0 || n1 > 0.0 || n2 > 0.0 || n3 > 0.0)) {
+                        m.na[0] = n0;
+                        m.na[1] = n1;
+                        m.na[2] = n2;
+                        m.na[3] = n3;
+                        // the fold below, as literal steps of the next iterations
+                        if (good < B && m.lim >= 1) m.lit = guess > good + 1.0 ? FOLD_MAX : 1;
+                        PT_MREG(adv_end);
+                        return M_RUNNING;
+                    }
                     if (n0 > 0.0) m.t = advance(m.t, s, n0);
                     if (n1 > 0.0) m.px = advance(m.px, cx, n1);
                     if (n2 > 0.0) m.py = advance(m.py, cy, n2);
                     if (n3 > 0.0) m.pz = advance(m.pz, cz, n3);
-#else
-                    m.t = advance(m.t, s, good);
-                    m.px = advance(m.px, cx, good);
-                    m.py = advance(m.py, cy, good);
-                    m.pz = advance(m.pz, cz, good);
-#endif
                     m.na[0] = m.na[1] = m.na[2] = m.na[3] = 0.0;
                     m.adv = 0;
                     m.r = shape_f_k<FK>(m.F, m.px, m.py, m.pz);
                     PT_MREG(adv_end);
                     // a prefix that stopped short of B ends just before the
                     // crossing: take that literal step in this iteration
-                    if (PT_FOLD_LIT && good < B && m.lim >= 1) {
+                    if (good < B && m.lim >= 1) {
                         // more than one when the predicted crossing is past the first
-                        nlit = guess > good + 1.0 ? PT_FOLD_MAX : 1;
+                        nlit = guess > good + 1.0 ? FOLD_MAX : 1;
                         goto literal;
                     }
                 }
@@ -879,7 +831,7 @@ literal:
             return m.pass >= m.passes ? M_DONE : M_RUNNING;
         }
         m.r = next;
-        if (PT_FOLD_MAX <= 1 || --nlit <= 0 || m.lim < 1.0) return M_RUNNING;
+        if (--nlit <= 0 || m.lim < 1.0) return M_RUNNING;
     }
 }
 
@@ -887,9 +839,9 @@ literal:
 // shared advance region and at most K binade segments per coordinate per
 // iteration, resumed in later iterations: slower for K = 2, 3, 4 and 64 —
 // DESIGN.md §3.2 — so a proven block's advance completes in its iteration.)
-template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY, bool DEFER = false>
 PT_HD int march_step(MarchState &m, MarchStats *st) {
-    return march_iter<STATS, INLINE_ADV, FK>(m, st);
+    return march_iter<STATS, INLINE_ADV, FK, DEFER>(m, st);
 }
 
 // What the next march_iter call will do, for wave-level phase scheduling

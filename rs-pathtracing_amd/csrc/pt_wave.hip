@@ -42,12 +42,18 @@
 #ifdef PT_MARCH_REGIONS
 // Tuning builds only: wave wall-clock (s_memtime) spent in each region of
 // the march kernel (pt_march.hpp's PT_MREG points), as seen by the wave's
-// first active lane, summed over all waves (pt_march_regions).
+// first active lane, summed over all waves, the same weighted by the lanes
+// active at the region's start, and per profiling point of pt_march.hpp
+// (PT_MPROF: one per segment, halving level, literal add, ...) the wave
+// passes and the lanes active in them (pt_march_regions).
 namespace pt {
 namespace mreg {
 enum { R_ITER, R_POLY, R_PREFIX, R_HALVE, R_ADV, R_LIT, R_REFILL, R_TOTAL, R_N };
-__device__ unsigned long long g_acc[R_N];
-__shared__ unsigned long long t0[4][R_N], acc[4][R_N];
+enum { P_iters, P_lin_init, P_lit_adds, P_advance_loops, P_evals, P_sir_inside, P_lin_fail_zero, P_lin_fail_q,
+       P_lin_fail_tie, P_lin_fail_zone, P_N };
+constexpr int G_N = 2 * R_N + 2 * P_N;
+__device__ unsigned long long g_acc[G_N];
+__shared__ unsigned long long t0[4][R_N], acc[4][R_N], accl[4][R_N], n0[4][R_N], pw[4][P_N], pl[4][P_N];
 __device__ __forceinline__ unsigned long long now() {
     __builtin_amdgcn_sched_barrier(0);
     const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -59,10 +65,25 @@ __device__ __forceinline__ bool leader() {
     return lane == (uint32_t)__builtin_ctzll(__ballot(1));
 }
 __device__ __forceinline__ void begin(int r) {
-    if (leader()) t0[threadIdx.x >> 6][r] = now();
+    const unsigned long long m = __ballot(1);
+    if (leader()) {
+        t0[threadIdx.x >> 6][r] = now();
+        n0[threadIdx.x >> 6][r] = __popcll(m);
+    }
 }
 __device__ __forceinline__ void end(int r) {
-    if (leader()) acc[threadIdx.x >> 6][r] += now() - t0[threadIdx.x >> 6][r];
+    if (leader()) {
+        const unsigned long long dt = now() - t0[threadIdx.x >> 6][r];
+        acc[threadIdx.x >> 6][r] += dt;
+        accl[threadIdx.x >> 6][r] += dt * n0[threadIdx.x >> 6][r];
+    }
+}
+__device__ __forceinline__ void prof(int k) {
+    const unsigned long long m = __ballot(1);
+    if (leader()) {
+        pw[threadIdx.x >> 6][k] += 1;
+        pl[threadIdx.x >> 6][k] += __popcll(m);
+    }
 }
 __device__ __forceinline__ void poly_begin() { begin(R_POLY); }
 __device__ __forceinline__ void poly_end() { end(R_POLY); }
@@ -76,6 +97,7 @@ __device__ __forceinline__ void lit_begin() { begin(R_LIT); }
 }  // namespace mreg
 }  // namespace pt
 #define PT_MREG(what) pt::mreg::what()
+#define PT_MPROF(field) (pt::mreg::prof(pt::mreg::P_##field))
 #endif
 
 #include "pt_device.hpp"
@@ -121,7 +143,7 @@ struct WfView {
     uint8_t *status;  // per output position of a bounce: bit 0 path alive, bit 1 needs a march, bit 2 long march
     uint32_t *list, *mq;  // positions (in `out` of the previous / current bounce) of the live paths and march jobs
     // march jobs pre-selected by the bounce kernel (scenes with one ray-marched
-    // shape, PT_WF_PRESELECT): object-space ray and bound interval per position,
+    // shape): object-space ray and bound interval per position,
     // 64 B each (o, d, start, end); null when the march kernel selects itself
     double2 *jo;
     uint32_t *cnt;  // per iteration: [0] live-list count, [1] march-queue count, [2..3] unused
@@ -198,40 +220,24 @@ __device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3
 // and its attenuation-stack depth; the per-pixel reduce unwinds the stack
 // (the recursion's products, in its order) when it sums the chunk's samples,
 // so the bounce kernel's waves never wait for the unwind's dependent loads.
-#ifndef PT_WF_NT_END
-#define PT_WF_NT_END 1  // non-temporal too (read once, by the chunk's reduce): iso bounce -0.6 ms, C2 +0.4 %
-#endif
+// Non-temporal (read once, by the chunk's reduce): iso bounce -0.6 ms, C2 +0.4 %.
 __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const MemStack &stk, V3 leaf) {
-    if (PT_WF_NT_END) {
-        __builtin_nontemporal_store(leaf.x, v.rx + id);
-        __builtin_nontemporal_store(leaf.y, v.ry + id);
-        __builtin_nontemporal_store(leaf.z, v.rz + id);
-        __builtin_nontemporal_store((uint32_t)stk.n, v.fin + id);
-        return;
-    }
-    v.rx[id] = leaf.x;
-    v.ry[id] = leaf.y;
-    v.rz[id] = leaf.z;
-    v.fin[id] = (uint32_t)stk.n;
+    __builtin_nontemporal_store(leaf.x, v.rx + id);
+    __builtin_nontemporal_store(leaf.y, v.ry + id);
+    __builtin_nontemporal_store(leaf.z, v.rz + id);
+    __builtin_nontemporal_store((uint32_t)stk.n, v.fin + id);
 }
 
-// A live path's state at output position k.  PT_WF_NT: non-temporal stores
-// (the state is read back only by the next bounce, after 1.8 GB of other
-// traffic: no cache level holds it that long).
-#ifndef PT_WF_NT
-#define PT_WF_NT 1  // C2: iso bounce 216.2 -> 211.5 ms, 1792 -> 1814 M samples/s (non-temporal loads: slower)
-#endif
+// A live path's state at output position k: non-temporal stores (the state
+// is read back only by the next bounce, after 1.8 GB of other traffic: no
+// cache level holds it that long; C2 iso bounce 216.2 -> 211.5 ms, 1792 ->
+// 1814 M samples/s; non-temporal loads were slower).
 template <typename T>
 __device__ __forceinline__ void st_path(T *p, T x) {
-    if (PT_WF_NT) __builtin_nontemporal_store(x, p);
-    else *p = x;
+    __builtin_nontemporal_store(x, p);
 }
-#ifndef PT_WF_NTL
-#define PT_WF_NTL 0  // non-temporal path-state loads in the bounce kernel
-#endif
 template <typename T>
 __device__ __forceinline__ T ld_path(const T *p) {
-    if (PT_WF_NTL) return __builtin_nontemporal_load(p);
     return *p;
 }
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
@@ -265,12 +271,9 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
     *y = ty * TILE + (((w >> 1) << 3) | (l >> 3));
 }
 
-#ifndef PT_WF_BPL
-#define PT_WF_BPL 1  // bounces a path may take per bounce launch while it needs no march
-#endif
-#ifndef PT_WF_PREDICT
-#define PT_WF_PREDICT 4  // points along a march job's chord whose sign of f predicts a hit (queue order only)
-#endif
+// points along a march job's chord whose sign of f predicts a hit (queue
+// order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
+constexpr int WF_PREDICT = 4;
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
 #endif
@@ -338,12 +341,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 PT_BSTAMP(1)
             }
         }
-        // Up to PT_WF_BPL bounces of this path: shade the pending hit (the
-        // camera ray has none), trace the new ray; go on while the path lives
-        // and no marched shape's bound starts before its best hit.
+        // One bounce of this path: shade the pending hit (the camera ray has
+        // none), trace the new ray, and find whether a marched shape's bound
+        // starts before its best hit.  (Up to 2-3 bounces per launch for paths
+        // needing no march measured +0.8 % / -2.5 %, round 2.)
         bool need_march = false, long_job = false;
-        for (int b = 0; live; b++) {
-            if (!FIRST || b > 0) {
+        if (live) {
+            if (!FIRST) {
                 V3 leaf;
                 const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
                 PT_BSTAMP(2)
@@ -353,9 +357,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     end_path(v, id, stk, leaf);
                     live = false;
                     PT_BSTAMP(3)
-                    break;
                 }
             }
+        }
+        if (live) {
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             best = __builtin_inf();
             who = -1;
@@ -372,33 +377,24 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
                 if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
-                    if (!PT_WF_NT) {
-                        double2 *j = v.jo + (size_t)i * 4;
-                        j[0] = make_double2(o.x, o.y);
-                        j[1] = make_double2(o.z, d.x);
-                        j[2] = make_double2(d.y, d.z);
-                        j[3] = make_double2(st, en);
-                    } else {
-                    double *j = (double *)(v.jo + (size_t)i * 4);
-                    st_path(j + 0, o.x);
-                    st_path(j + 1, o.y);
-                    st_path(j + 2, o.z);
-                    st_path(j + 3, d.x);
-                    st_path(j + 4, d.y);
-                    st_path(j + 5, d.z);
-                    st_path(j + 6, st);
-                    st_path(j + 7, en);
-                    }
+                    // the 64 B record in four 16-byte non-temporal stores (as eight 8-byte ones: the
+                    // same time; structure of arrays: slower, round 3 jo2)
+                    typedef double d2v __attribute__((ext_vector_type(2)));
+                    d2v *j = (d2v *)(v.jo + (size_t)i * 4);
+                    __builtin_nontemporal_store((d2v){o.x, o.y}, j + 0);
+                    __builtin_nontemporal_store((d2v){o.z, d.x}, j + 1);
+                    __builtin_nontemporal_store((d2v){d.y, d.z}, j + 2);
+                    __builtin_nontemporal_store((d2v){st, en}, j + 3);
                     // queue order only: a march that will cross the surface (a hit: ~3x
                     // the iterations of a miss) is predicted by the sign of f at the bound
-                    // entry and at PT_WF_PREDICT points along the chord (inside is f < 0;
+                    // entry and at WF_PREDICT points along the chord (inside is f < 0;
                     // measured on captured cornell jobs: every predicted job a hit, 0.2 %
                     // of the others)
                     long_job = march::shape_f_k<FK>(dev::shape_params(S), o.x + d.x * st, o.y + d.y * st,
                                                     o.z + d.z * st) < 0.0;
-                    const double dt = (en - st) * (1.0 / PT_WF_PREDICT);
+                    const double dt = (en - st) * (1.0 / WF_PREDICT);
 #pragma unroll
-                    for (int q = 0; q < PT_WF_PREDICT; q++) {
+                    for (int q = 0; q < WF_PREDICT; q++) {
                         const double tq = st + dt * (q + 0.5);
                         long_job = long_job || march::shape_f_k<FK>(dev::shape_params(S), o.x + d.x * tq,
                                                                     o.y + d.y * tq, o.z + d.z * tq) < 0.0;
@@ -406,12 +402,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 }
             }
             PT_BSTAMP(5)
-            if (need_march || b + 1 >= PT_WF_BPL) break;
         }
-#ifndef PT_WF_STORE_ALL
-#define PT_WF_STORE_ALL 1  // every input position's state is written (ended paths too: whole lines)
-#endif
-        if (live || (PT_WF_STORE_ALL && i < count))
+        // every input position's state is written (ended paths too: whole lines; storeab)
+        if (i < count)
             store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
         if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
@@ -725,29 +718,11 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 // passes) is staged in LDS once per workgroup.  A job is trace_pixel's
 // SELECT/MARCH loop over the marched shapes for one path; (best, who) go back
 // to the path, which the next bounce kernel reads from the live list.
-#ifndef PT_WF_VOTE
-#define PT_WF_VOTE 0
-#endif
-#ifndef PT_WF_SEL_BATCH
-#define PT_WF_SEL_BATCH 0
-#endif
-#ifndef PT_WF_UNITS
-#define PT_WF_UNITS 1
-#endif
-#ifndef PT_WF_PRESELECT
-#define PT_WF_PRESELECT 1  // bounce kernel hands the march its object-space ray and bound (one marched shape): C2 +9 % (iso march 340 -> 275 ms, bounce 248 -> 256)
-#endif
-#ifndef PT_WF_BOUNCE_CAP
-#define PT_WF_BOUNCE_CAP 8192  // bounce grid (blocks) after the first iteration; threads loop over the live list
-#endif
-#ifndef PT_WF_MNT
-#define PT_WF_MNT 0  // non-temporal march result stores
-#endif
-#ifndef PT_WF_STORE_LATE
-#define PT_WF_STORE_LATE 1  // march: a finished job's results are stored after the next job's loads have landed
-#endif
-#ifndef PT_WF_INLINE_ADV
-#define PT_WF_INLINE_ADV (PT_WF_VOTE == 0)  // a proven block's exact advance in the same trip (0: PT_ADV_ROUNDS per trip)
+// Measured and dropped (profiles/r2/ab_round2_experiments.txt): a per-wave phase vote,
+// batched job switches, several march units per trip, non-temporal result stores.
+constexpr uint32_t WF_BOUNCE_CAP = 8192;  // bounce grid (blocks) after the first iteration; threads loop over the live list
+#ifndef PT_WF_ADV_DEFER
+#define PT_WF_ADV_DEFER 0  // lanes of a wave whose long block advances are walked together (0: in-line)
 #endif
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 4  // waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs, 20 B: 1273; 3: 1261)
@@ -838,8 +813,11 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         }
     };
 #ifdef PT_MARCH_REGIONS
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < mreg::R_N; k++) mreg::t0[threadIdx.x >> 6][k] = mreg::acc[threadIdx.x >> 6][k] = 0;
+    if ((threadIdx.x & 63) == 0) {
+        for (int k = 0; k < mreg::R_N; k++)
+            mreg::t0[threadIdx.x >> 6][k] = mreg::acc[threadIdx.x >> 6][k] = mreg::accl[threadIdx.x >> 6][k] = 0;
+        for (int k = 0; k < mreg::P_N; k++) mreg::pw[threadIdx.x >> 6][k] = mreg::pl[threadIdx.x >> 6][k] = 0;
+    }
     const unsigned long long t_kernel = mreg::now();
 #endif
     if (have) start_job(pos(q));
@@ -871,40 +849,34 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             mask_prev = mk;
         }
         if (!have) continue;
-#if PT_WF_SEL_BATCH
-        // Job ends/switches load the next job's ray from HBM, a wait the
-        // whole wave pays: lanes needing one wait until >= PT_WF_SEL_BATCH of
-        // them do (or nothing else runs), so one wait serves many lanes.
+#if PT_WF_ADV_DEFER
+        // Batched long advances: a lane whose proven block needs more than one
+        // binade segment in some coordinate (a coordinate crossing zero walks
+        // ~2 log2(|x| / |c|) of them) waits until PT_WF_ADV_DEFER lanes of its
+        // wave do, or until every lane with a job does, and they walk their
+        // segments together; in-line, each such walk ran with ~3 lanes active.
         {
-            const bool want_sel = !marching;
-            const uint64_t msel = __ballot(want_sel);
-            if (want_sel && __popcll(msel) < PT_WF_SEL_BATCH && msel != __ballot(true)) continue;
+            const bool pend = marching && ms.adv;
+            const uint64_t mp = __ballot(pend), mh = __ballot(true);
+            if (pend && __popcll(mp) < PT_WF_ADV_DEFER && mp != mh) continue;
         }
 #endif
-#if PT_WF_VOTE
-        // Phase vote: the wave runs one kind of work per trip, cheapest
-        // first; the proof runs only when every live lane waits for it.
-        const int ph = marching ? march::march_phase(ms) : 3;
-        const uint64_t m_cheap = __ballot(ph == march::MP_CHEAP), m_sel = __ballot(ph == 3),
-                       m_adv = __ballot(ph == march::MP_ADV);
-        const int run = m_cheap ? march::MP_CHEAP : (m_sel ? 3 : (m_adv ? march::MP_ADV : march::MP_PROOF));
-        if (ph != run) continue;
-#endif
-        // up to PT_WF_UNITS units of work per trip (a march iteration, a
-        // select step, a job switch): short jobs do not pay a trip per step
-        for (int unit = 0; unit < PT_WF_UNITS && have; unit++) {
+        // one unit of work per trip: a march iteration, a select step or a job switch
+        {
             bool done = false;
             if (marching) {
 #ifdef PT_MARCH_REGIONS
                 mreg::begin(mreg::R_ITER);
-                const int st = march::march_step<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
+                const int st = march::march_step<false, true, FK, (PT_WF_ADV_DEFER > 0)>(ms, &mst);
                 mreg::end(mreg::R_ITER);
                 if (mreg::leader() && mreg::t0[threadIdx.x >> 6][mreg::R_LIT]) {  // a literal loop ran: close it
-                    mreg::acc[threadIdx.x >> 6][mreg::R_LIT] += mreg::now() - mreg::t0[threadIdx.x >> 6][mreg::R_LIT];
+                    const unsigned long long dt = mreg::now() - mreg::t0[threadIdx.x >> 6][mreg::R_LIT];
+                    mreg::acc[threadIdx.x >> 6][mreg::R_LIT] += dt;
+                    mreg::accl[threadIdx.x >> 6][mreg::R_LIT] += dt * mreg::n0[threadIdx.x >> 6][mreg::R_LIT];
                     mreg::t0[threadIdx.x >> 6][mreg::R_LIT] = 0;
                 }
 #else
-                const int st = march::march_step<false, PT_WF_INLINE_ADV != 0, FK>(ms, &mst);
+                const int st = march::march_step<false, true, FK, (PT_WF_ADV_DEFER > 0)>(ms, &mst);
 #endif
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);
@@ -940,26 +912,16 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
 #endif
                 // vmcnt counts loads and stores in issue order: a store issued
                 // before the next job's loads makes the wait for those loads a
-                // wait for the store's completion too
+                // wait for the store's completion too, so the finished job's
+                // results are stored after the next job's loads are issued
                 const uint32_t fid = cur.id;
                 const double fbest = cur.best;
                 const int fwho = cur.who;
-                if (!PT_WF_STORE_LATE) {
-                    v.out.t()[fid] = fbest;
-                    v.out.who()[fid] = fwho;
-                }
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
                 if (have) start_job(pos(q));
-                if (PT_WF_STORE_LATE) {
-#if PT_WF_MNT
-                    __builtin_nontemporal_store(fbest, v.out.t() + fid);
-                    __builtin_nontemporal_store((int32_t)fwho, v.out.who() + fid);
-#else
-                    v.out.t()[fid] = fbest;
-                    v.out.who()[fid] = fwho;
-#endif
-                }
+                v.out.t()[fid] = fbest;
+                v.out.who()[fid] = fwho;
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
@@ -972,8 +934,17 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     }
 #ifdef PT_MARCH_REGIONS
     if ((threadIdx.x & 63) == 0) {
-        mreg::acc[threadIdx.x >> 6][mreg::R_TOTAL] = mreg::now() - t_kernel;
-        for (int k = 0; k < mreg::R_N; k++) atomicAdd(&mreg::g_acc[k], mreg::acc[threadIdx.x >> 6][k]);
+        const int w = threadIdx.x >> 6;
+        mreg::acc[w][mreg::R_TOTAL] = mreg::now() - t_kernel;
+        mreg::accl[w][mreg::R_TOTAL] = 0;
+        for (int k = 0; k < mreg::R_N; k++) {
+            atomicAdd(&mreg::g_acc[k], mreg::acc[w][k]);
+            atomicAdd(&mreg::g_acc[mreg::R_N + k], mreg::accl[w][k]);
+        }
+        for (int k = 0; k < mreg::P_N; k++) {
+            atomicAdd(&mreg::g_acc[2 * mreg::R_N + k], mreg::pw[w][k]);
+            atomicAdd(&mreg::g_acc[2 * mreg::R_N + mreg::P_N + k], mreg::pl[w][k]);
+        }
     }
 #endif
     if (DIAG && (threadIdx.x & 63) == 0) {
@@ -1283,8 +1254,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     if (ws->used && (e = hipStreamWaitEvent(st, ws->done, 0)) != hipSuccess) return e;
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
     const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
-    // pre-selected march jobs: one marched shape, PT_WF_PRESELECT
-    const bool presel = PT_WF_PRESELECT && sc.nmarch == 1 && !ws->diag;
+    // pre-selected march jobs (one marched shape): the bounce kernel hands the march its object-space ray
+    // and bound (C2 +9 %: iso march 340 -> 275 ms, bounce 248 -> 256, round 1)
+    const bool presel = sc.nmarch == 1 && !ws->diag;
     // two path-state sets (8 + 3 words per path each), sample radiances, lists, end depths
     const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 8) * 3 +
                               (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 3 +
@@ -1397,7 +1369,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 v.in = sl[j].set[it & 1];
                 v.out = sl[j].set[(it + 1) & 1];
                 uint32_t bb = (paths + 255) / 256;
-                if (bb > PT_WF_BOUNCE_CAP) bb = PT_WF_BOUNCE_CAP;
+                if (bb > WF_BOUNCE_CAP) bb = WF_BOUNCE_CAP;
                 if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
@@ -1426,6 +1398,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (sc.nmarch == 0) continue;  // no ray-marched shape: the march queue is always empty
+#ifdef PT_ABL_NOMARCH
+                continue;  // timing ablation only (not exact): the march kernel's share of the frame
+#endif
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)
@@ -1473,7 +1448,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
 extern "C" int pt_march_regions(unsigned long long *out, int clear) {
     if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(mreg::g_acc), sizeof(mreg::g_acc)) != hipSuccess) return -1;
     if (clear) {
-        static const unsigned long long z[mreg::R_N] = {};
+        static const unsigned long long z[mreg::G_N] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(mreg::g_acc), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -55,6 +55,12 @@ stall)
         SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT \
         -- python3 $R/bench.py "$@" > $OUT/stall.log 2>&1
     python3 scripts/pmc_summary.py $OUT/stall > $OUT/stall_summary.txt ;;
+cache)  # L2 hit rate and vector-memory request mix per kernel (one pass; list the names with rocprofv3 -L)
+    prof --kernel-trace --output-format csv -d $OUT/cache -o p --pmc ${CACHE_PMC:-TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TA_BUSY_avr} \
+        -- python3 $R/bench.py "$@" > $OUT/cache.log 2>&1
+    python3 scripts/pmc_summary.py $OUT/cache > $OUT/cache_summary.txt ;;
+list)
+    (cd /tmp && timeout -s KILL 120 rocprofv3 -L) > $OUT/counters.txt 2>&1 || true ;;
 evidence)
     bash scripts/gpu.sh tests $tag
     bash scripts/gpu.sh smoke $tag

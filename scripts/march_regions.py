@@ -18,7 +18,9 @@ L = pt.lib()
 f = L.pt_march_regions
 f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 names = ["iter", "poly+guess", "prefix", "halvings", "advance", "literal", "refill", "total"]
-buf = (C.c_ulonglong * len(names))()
+pnames = ["iters", "lin_init", "lit_adds", "advance_loops", "evals", "sir_inside", "lin_fail_zero", "lin_fail_q",
+          "lin_fail_tie", "lin_fail_zone"]
+buf = (C.c_ulonglong * (2 * len(names) + 2 * len(pnames)))()
 sc = pt.Scene.from_json(open("scenes/cornell_box.json").read(), seed=1)
 r = pt.HipRenderer(sc, device=0, depth=8)
 r.set_option("wf_slots", 1)
@@ -33,5 +35,12 @@ torch.cuda.synchronize()
 f(buf, 0)
 tot = buf[7]
 print("march kernel wave time by region (%% of total wave cycles %.4g), %dx%d %d spp" % (tot, W, H, spp))
-for n, x in zip(names, buf):
-    print("  %-11s %6.1f%%" % (n, 100.0 * x / max(1, tot)))
+R, P = len(names), len(pnames)
+for k, n in enumerate(names):
+    x, xl = buf[k], buf[R + k]
+    print("  %-11s %6.1f%%   lanes active at its start %5.1f of 64" % (n, 100.0 * x / max(1, tot), xl / max(1, x)))
+print("profiling points: wave passes, mean lanes per pass (pt_march.hpp PT_MPROF)")
+for k, n in enumerate(pnames):
+    w, l = buf[2 * R + k], buf[2 * R + P + k]
+    if w:
+        print("  %-14s %12d passes  %5.1f lanes" % (n, w, l / w))

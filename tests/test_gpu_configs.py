@@ -104,6 +104,8 @@ def test_c5_synthetic_100k_spheres(pt, c5):
     ref = osc.render(160, 90, 2, 8, 2)
     assert np.array_equal(img, ref)
     assert img.mean() > 0.05
+    r.set_option("bvh_leaf", 3)  # the BVH rebuilt with 3 shapes per leaf: the same closest hits
+    assert np.array_equal(r.render(cam, pt.ImageParams(160, 90), 2, seed=2), ref)
 
 
 def test_shard_pixels_matches_device_deal(pt, cornell):

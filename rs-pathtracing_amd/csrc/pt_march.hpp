@@ -691,12 +691,7 @@ PT_HD void march_advance(MarchState &m, double cx, double cy, double cz) {
 // One iteration of the march loop: a proven jump, or one literal step (after a
 // failed proof).  M_DONE: the passes ended (the caller applies the final
 // t-in-[min_t, max_t] test); M_MISS: t left [start, end].
-// DEFER (with INLINE_ADV): a coordinate whose advance does not end with its
-// first binade segment leaves the rest for later: the iteration returns with
-// m.adv set (and the fold's literal steps in m.lit), and a later iteration
-// runs march_advance.  The caller decides when (wf_march batches the lanes of
-// a wave that wait for one); the operations on the job are the same either way.
-template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY, bool DEFER = false>
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
 PT_HD int march_iter(MarchState &m, MarchStats *st) {
     PT_MPROF(iters);
     int nlit = 1;
@@ -775,16 +770,6 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
                     seg_step(m.px, cx, n1);
                     seg_step(m.py, cy, n2);
                     seg_step(m.pz, cz, n3);
-                    if (DEFER && (n0 > 0.0 || n1 > 0.0 || n2 > 0.0 || n3 > 0.0)) {
-                        m.na[0] = n0;
-                        m.na[1] = n1;
-                        m.na[2] = n2;
-                        m.na[3] = n3;
-                        // the fold below, as literal steps of the next iterations
-                        if (good < B && m.lim >= 1) m.lit = guess > good + 1.0 ? FOLD_MAX : 1;
-                        PT_MREG(adv_end);
-                        return M_RUNNING;
-                    }
                     if (n0 > 0.0) m.t = advance(m.t, s, n0);
                     if (n1 > 0.0) m.px = advance(m.px, cx, n1);
                     if (n2 > 0.0) m.py = advance(m.py, cy, n2);
@@ -839,9 +824,9 @@ literal:
 // shared advance region and at most K binade segments per coordinate per
 // iteration, resumed in later iterations: slower for K = 2, 3, 4 and 64 —
 // DESIGN.md §3.2 — so a proven block's advance completes in its iteration.)
-template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY, bool DEFER = false>
+template <bool STATS, bool INLINE_ADV = true, int FK = F_ANY>
 PT_HD int march_step(MarchState &m, MarchStats *st) {
-    return march_iter<STATS, INLINE_ADV, FK, DEFER>(m, st);
+    return march_iter<STATS, INLINE_ADV, FK>(m, st);
 }
 
 // What the next march_iter call will do, for wave-level phase scheduling

@@ -721,9 +721,6 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 // Measured and dropped (profiles/r2/ab_round2_experiments.txt): a per-wave phase vote,
 // batched job switches, several march units per trip, non-temporal result stores.
 constexpr uint32_t WF_BOUNCE_CAP = 8192;  // bounce grid (blocks) after the first iteration; threads loop over the live list
-#ifndef PT_WF_ADV_DEFER
-#define PT_WF_ADV_DEFER 0  // lanes of a wave whose long block advances are walked together (0: in-line)
-#endif
 #ifndef PT_WF_MARCH_WAVES
 #define PT_WF_MARCH_WAVES 4  // waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs, 20 B: 1273; 3: 1261)
 #endif
@@ -849,25 +846,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             mask_prev = mk;
         }
         if (!have) continue;
-#if PT_WF_ADV_DEFER
-        // Batched long advances: a lane whose proven block needs more than one
-        // binade segment in some coordinate (a coordinate crossing zero walks
-        // ~2 log2(|x| / |c|) of them) waits until PT_WF_ADV_DEFER lanes of its
-        // wave do, or until every lane with a job does, and they walk their
-        // segments together; in-line, each such walk ran with ~3 lanes active.
-        {
-            const bool pend = marching && ms.adv;
-            const uint64_t mp = __ballot(pend), mh = __ballot(true);
-            if (pend && __popcll(mp) < PT_WF_ADV_DEFER && mp != mh) continue;
-        }
-#endif
         // one unit of work per trip: a march iteration, a select step or a job switch
         {
             bool done = false;
             if (marching) {
 #ifdef PT_MARCH_REGIONS
                 mreg::begin(mreg::R_ITER);
-                const int st = march::march_step<false, true, FK, (PT_WF_ADV_DEFER > 0)>(ms, &mst);
+                const int st = march::march_step<false, true, FK>(ms, &mst);
                 mreg::end(mreg::R_ITER);
                 if (mreg::leader() && mreg::t0[threadIdx.x >> 6][mreg::R_LIT]) {  // a literal loop ran: close it
                     const unsigned long long dt = mreg::now() - mreg::t0[threadIdx.x >> 6][mreg::R_LIT];
@@ -876,7 +861,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                     mreg::t0[threadIdx.x >> 6][mreg::R_LIT] = 0;
                 }
 #else
-                const int st = march::march_step<false, true, FK, (PT_WF_ADV_DEFER > 0)>(ms, &mst);
+                const int st = march::march_step<false, true, FK>(ms, &mst);
 #endif
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);

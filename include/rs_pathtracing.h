@@ -275,7 +275,7 @@ int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
 
 /* Diagnostic of the wavefront kernels: returns (and clears) the counters
- * accumulated since the last call into out[min(n, 48)] — the march kernel's
+ * accumulated since the last call into out[min(n, 64)] — the march kernel's
  * trips and s_memtime cycles per mix of lane phases (16 + 16), lanes per
  * phase (4), then the bounce kernel's cycles per section (list load, state
  * loads, shade, unwind, trace, march pre-check, stores; each section ended by

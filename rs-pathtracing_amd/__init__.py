@@ -482,8 +482,8 @@ def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
 
 def wave_diag(renderer: "HipRenderer", enable: bool = True):
     """Read-and-clear the wavefront march kernel's phase diagnostics (pt_wave_diag)."""
-    out = (C.c_uint64 * 48)()
-    _check(lib().pt_wave_diag(renderer._h, 1 if enable else 0, out, 48))
+    out = (C.c_uint64 * 64)()
+    _check(lib().pt_wave_diag(renderer._h, 1 if enable else 0, out, 64))
     return list(out)
 
 

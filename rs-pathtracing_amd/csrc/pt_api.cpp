@@ -980,9 +980,9 @@ int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
     HIP_TRY(hipSetDevice(r->device()));
     HIP_TRY(hipStreamSynchronize(r->stream()));
-    if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 48 ? n : 48) * 8, hipMemcpyDeviceToHost));
-    if (enable && !r->gpus[0].ws.diag) HIP_TRY(hipMalloc(&r->gpus[0].ws.diag, 48 * 8));
-    if (r->gpus[0].ws.diag) HIP_TRY(hipMemset(r->gpus[0].ws.diag, 0, 48 * 8));
+    if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 64 ? n : 64) * 8, hipMemcpyDeviceToHost));
+    if (enable && !r->gpus[0].ws.diag) HIP_TRY(hipMalloc(&r->gpus[0].ws.diag, 64 * 8));
+    if (r->gpus[0].ws.diag) HIP_TRY(hipMemset(r->gpus[0].ws.diag, 0, 64 * 8));
     if (!enable && r->gpus[0].ws.diag) {
         HIP_TRY(hipFree(r->gpus[0].ws.diag));
         r->gpus[0].ws.diag = nullptr;

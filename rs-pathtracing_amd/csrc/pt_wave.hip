@@ -290,6 +290,27 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
     const uint32_t count = FIRST ? v.ns * v.npix : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
+#ifdef PT_BOUNCE_LANES
+    // Tuning builds only (with the diag build): wave cycles between
+    // consecutive stamps, charged to the section the stamp ends and weighted
+    // by the lanes active at it, by the wave's first active lane (no forced
+    // waits): where the bounce's lanes idle.
+    __shared__ unsigned long long bl_t0[4], bl_acc[4][7], bl_lan[4][7];
+    if (DIAG && (threadIdx.x & 63) == 0) {
+        bl_t0[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+        for (int k = 0; k < 7; k++) bl_acc[threadIdx.x >> 6][k] = bl_lan[threadIdx.x >> 6][k] = 0;
+    }
+#define PT_BSTAMP(k)                                                                              \
+    if (DIAG) {                                                                                   \
+        const unsigned long long m_ = __ballot(1);                                               \
+        if (lane_id() == (uint32_t)__builtin_ctzll(m_)) {                                        \
+            const unsigned long long n_ = __builtin_amdgcn_s_memtime(), d_ = n_ - bl_t0[threadIdx.x >> 6]; \
+            bl_acc[threadIdx.x >> 6][k] += d_;                                                   \
+            bl_lan[threadIdx.x >> 6][k] += d_ * __popcll(m_);                                    \
+            bl_t0[threadIdx.x >> 6] = n_;                                                        \
+        }                                                                                         \
+    }
+#else
 #define PT_BSTAMP(k)                                                \
     if (DIAG) {                                                     \
         __builtin_amdgcn_s_waitcnt(0);                              \
@@ -297,6 +318,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         dsec[k] += n_ - tst;                                        \
         tst = n_;                                                   \
     }
+#endif
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         if (DIAG) tst = __builtin_amdgcn_s_memtime();
         const uint32_t i = base + threadIdx.x;
@@ -410,8 +432,16 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
+#ifdef PT_BOUNCE_LANES
+    if (DIAG && (threadIdx.x & 63) == 0)
+        for (int k = 0; k < 7; k++) {
+            atomicAdd(&diag[36 + k], bl_acc[threadIdx.x >> 6][k]);
+            atomicAdd(&diag[48 + k], bl_lan[threadIdx.x >> 6][k]);
+        }
+#else
     if (DIAG && (threadIdx.x & 63) == 0)
         for (int k = 0; k < 7; k++) atomicAdd(&diag[36 + k], dsec[k]);
+#endif
 }
 
 // Fused bounces (PT_WF_FUSED=1; measured slower, see fused_bounces()): a lane carries its path through as

@@ -80,8 +80,12 @@ NATIVE = ROOT / "tests" / "native"
 
 
 def abi_check_bin():
+    import fcntl
     import subprocess
-    subprocess.run(["make", "-s", "-C", str(NATIVE), "_build/abi_check"], check=True)
+    (NATIVE / "_build").mkdir(exist_ok=True)
+    with open(NATIVE / "_build" / ".lock", "w") as lk:  # pytest-xdist workers: one make at a time
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", str(NATIVE), "_build/abi_check"], check=True)
     return str(NATIVE / "_build" / "abi_check")
 
 

@@ -41,7 +41,7 @@ hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches);  // su
 // initial values from the PT_* environment variables named below, once, when
 // it is created; bench.py reports every knob that differs from its default.
 struct Tuning {
-    int engine = 0;                  // PT_ENGINE: 0 auto (wavefront iff the scene marches), 1 megakernel, 2 wavefront
+    int engine = 0;                  // PT_ENGINE: 0 auto (wavefront for a scene that marches or has textures / a Torus, and for any frame of >= 2^22 samples; else the megakernel), 1 megakernel, 2 wavefront
     int mega_waves = 4;              // PT_WAVES: megakernel register budget, waves per SIMD (2..5)
     int diag = 0;                    // PT_DIAG bit 0: skip ray-marched shapes (a timing ablation, not the reference)
     int wf_slots = 2;                // PT_WF_SLOTS: sample chunks in flight, one stream each (1..4)

@@ -187,10 +187,13 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking);
  * Same return values as pt_render_step. */
 int pt_render_step_rgba8(pt_renderer *r, double *rgb, uint8_t *rgba, int blocking);
 /* Renderer::stop_rendering (mod.rs:55): the frame in flight is abandoned.  No
- * further band is queued; the bands already queued (at most two, each about
- * 1/8 of the frame) still run, and the call returns once the device streams
- * have drained them.  Bands already copied by render_step stay valid; the
- * rest of the buffer is not written. */
+ * further band is queued, and the renderer's stop flag (host-mapped, read by
+ * every launch of the frame as it starts) turns the launches already queued
+ * into no-ops; the call returns once the device streams are idle, i.e. after
+ * the kernels that were running when it was called (milliseconds, not the
+ * seconds two whole bands take at 4K x 4096 spp).  Bands already copied by
+ * render_step stay valid; the rest of the buffer is not written.  Frames
+ * queued by pt_render_device / pt_render_frame_device are not affected. */
 int pt_render_stop(pt_renderer *r);
 
 /* ---- device-resident frame (benchmarks, multi-GPU) --------------------- */

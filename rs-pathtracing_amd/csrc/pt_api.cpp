@@ -108,6 +108,13 @@ struct pt_renderer {
     std::atomic<uint32_t> bands_queued{0};  // bands [0, n) are queued (their events recorded)
     std::atomic<int> feed_rc{0};            // the feeder's failure status (feed_err holds the message)
     std::string feed_err;
+    // The progressive frame's stop flag (FrameParams::stop), host-mapped and
+    // coherent so the kernels see pt_render_stop's store at once: while it is
+    // set, a queued launch of the frame does no work, so the stop returns
+    // after the launches already running instead of two whole bands.  Frames
+    // queued by pt_render_device / pt_render_frame_device carry no flag.
+    int *h_stop = nullptr;
+    const int *d_stop = nullptr;
 
     int device() const { return gpus[0].device; }
     hipStream_t stream() const { return gpus[0].stream; }
@@ -318,7 +325,7 @@ int upload_accel(GpuShare &g, const Accel &acc) {
     return PT_OK;
 }
 
-// Uploads the realized scene to one device and creates its stream and stop flag.
+// Uploads the realized scene to one device and creates its stream.
 int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const std::vector<DShape> &hs,
                const std::vector<DMaterial> &hm) {
     g.device = device;
@@ -566,6 +573,20 @@ int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t d
         return rc;
     }
     (void)hipSetDevice(devices[0]);
+    {
+        void *dp = nullptr;
+        hipError_t e = hipHostMalloc((void **)&r->h_stop, sizeof(int),
+                                     hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            __atomic_store_n(r->h_stop, 0, __ATOMIC_SEQ_CST);
+            e = hipHostGetDevicePointer(&dp, r->h_stop, 0);
+        }
+        if (e != hipSuccess) {
+            pt_renderer_destroy(r);
+            return hip_fail(e, "allocating the stop flag");
+        }
+        r->d_stop = (const int *)dp;
+    }
     *out = r;
     return PT_OK;
 }
@@ -666,6 +687,7 @@ void pt_renderer_destroy(pt_renderer *r) {
         if (r->d_gather) (void)hipFree(r->d_gather);
     }
     for (auto &g : r->gpus) free_share(g);
+    if (r->h_stop) (void)hipHostFree(r->h_stop);
     delete r;
 }
 
@@ -680,6 +702,7 @@ int pt_render_start(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h
     if (int rc = grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4)) return rc;
     if (int rc = frame_prologue(r, w, h)) return rc;
     r->frame = frame_params(r, *cam, w, h, spp, seed);
+    r->frame.stop = r->d_stop;
     // ~8 bands of whole tile rows: a band is one pass of the engine over
     // 1/8 of the frame, big enough to fill the device
     const uint32_t ty = tiles_y_of(h);
@@ -768,13 +791,18 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking) {
     return pt_render_step_rgba8(r, rgb, nullptr, blocking);
 }
 
-// Renderer::stop_rendering: the feeder queues no further band; the (at most
-// two) bands already queued drain; the frame is forgotten.
+// Renderer::stop_rendering: the feeder queues no further band and the stop
+// flag turns the frame's queued launches into no-ops, so the wait is for the
+// launches already running; the flag is cleared once the streams are idle
+// and the frame is forgotten.
 int pt_render_stop(pt_renderer *r) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
     r->stop_req.store(true);
+    const bool flag = r->started && r->h_stop;
+    if (flag) __atomic_store_n(r->h_stop, 1, __ATOMIC_SEQ_CST);
     join_feeder(r);
     int rc = sync_all(r);
+    if (flag) __atomic_store_n(r->h_stop, 0, __ATOMIC_SEQ_CST);
     release_bands(r);
     r->started = false;
     return rc;

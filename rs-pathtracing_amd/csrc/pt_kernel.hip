@@ -27,6 +27,12 @@ using dev::V3;
 // (__launch_bounds__' second argument): 2 -> <= 256 VGPRs, 3 -> <= 168, 4 -> <= 128, 5 -> <= 102.
 template <int NW, int WAVES, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
+    if (P.stop) {  // progressive frames: one read of the host-mapped stop flag per block
+        __shared__ int halt;
+        if (threadIdx.x == 0) halt = dev::stopped(P.stop);
+        __syncthreads();
+        if (halt) return;
+    }
     const uint32_t ti = P.tile_begin + blockIdx.x;  // index in this rank's tile list
     const uint32_t k = dev::tile_position(P.rank + ti * P.world, P.tiles_x, P.world);  // global tile id
     const uint32_t tx = k % P.tiles_x, ty = k / P.tiles_x;

@@ -88,7 +88,10 @@ struct FrameParams {
     uint64_t seed;
     uint32_t width, height, spp, depth;
     uint32_t rank, world, tiles_x, tile_begin;
-    uint32_t tile_count, compact, pad0, pad1;
+    uint32_t tile_count, compact;
+    // progressive frames: the renderer's stop flag in host-mapped memory
+    // (pt_render_stop sets it while it drains the queued launches); null: none
+    const int *stop;
 };
 
 // Work counters of the diagnostic (STATS) kernel build: the kernel's own event

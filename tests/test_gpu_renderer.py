@@ -4,8 +4,9 @@ drives it (src/bin/main.rs:262-290):
 * progressive, non-blocking render_step (step_by_step.rs:101-121): bands of a
   C2-size frame arrive while the rest is still rendering, and every band that
   has arrived already equals the oracle for its rows;
-* stop_rendering (mod.rs:55) abandons a frame in flight quickly and leaves
-  the renderer usable; the GUI's 1 spp -> 100 spp restart sequence;
+* stop_rendering (mod.rs:55) abandons a frame in flight quickly (the queued
+  launches see the stop flag and do no work) and leaves the renderer usable;
+  the GUI's 1 spp -> 100 spp restart sequence;
 * the display encode (main.rs:281-289) on the GPU equals the host encode and
   the reference's formula, fused into render_step_rgba8;
 * several devices behind one renderer (pt_renderer_create_multi): the tile
@@ -110,6 +111,54 @@ def test_gui_restart_sequence_and_stop(pt, cornell):
     t_full = time.perf_counter() - t0
     assert t_stop < 0.5 * t_full, (t_stop, t_full)
     sampled_rows_check(osc, buf, w, h, 100, np.arange(h), n=1024, seed=2)
+
+
+def test_stop_waits_only_for_running_launches(pt, cornell):
+    """A stop of a C3-size frame in mid-band: the stop flag turns the queued
+    launches (the rest of two bands of ~0.5 s each) into no-ops, so the call
+    returns after the kernels already running; the flag is clear again for the
+    next frame, which is exact."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h, spp = 3840, 2160, 1024
+    r.start_rendering(cam, pt.ImageParams(w, h), spp, seed=1)
+    time.sleep(0.8)
+    t0 = time.perf_counter()
+    r.stop_rendering()
+    t_stop = time.perf_counter() - t0
+    print("stop of a 3840x2160 1024 spp frame after 0.8 s: %.1f ms" % (t_stop * 1e3))
+    assert t_stop < 0.2, t_stop
+    w2, h2 = 320, 180
+    buf = np.zeros((w2 * h2, 3))
+    r.start_rendering(cam, pt.ImageParams(w2, h2), 4, seed=1)
+    assert r.render_step(buf, blocking=True)
+    assert np.array_equal(buf, osc.render(w2, h2, 4, 8, 1, threads=host_threads()))
+
+
+def test_stop_leaves_device_frames_alone(pt, cornell):
+    """A frame queued by render_device carries no stop flag: a progressive
+    frame started and stopped while it still runs does not cut it short."""
+    import torch
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    cam = ps.camera()
+    w, h, spp = 1920, 1080, 64
+    stream = torch.cuda.current_stream().cuda_stream
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    r.render_device(cam, w, h, spp, 3, 0, 1, frame.data_ptr(), stream)  # ~70 ms of work, queued
+    r.start_rendering(cam, pt.ImageParams(w, h), spp, seed=5)  # its bands wait for the workspace
+    r.stop_rendering()
+    torch.cuda.synchronize()
+    img = frame.view(-1, 3).cpu().numpy()
+    assert np.all(np.isfinite(img))
+    sampled_rows_check_seed(osc, img, w, h, spp, 3)
+
+
+def sampled_rows_check_seed(osc, img, w, h, spp, seed, n=1024):
+    rng = np.random.default_rng(seed)
+    px = np.unique(rng.integers(0, w * h, size=n).astype(np.uint32))
+    assert np.array_equal(img[px], osc.render(w, h, spp, 8, seed, pixels=px, threads=host_threads()))
 
 
 def test_restart_replaces_frame_in_flight(pt, cornell):

@@ -187,9 +187,10 @@ int pt_render_step(pt_renderer *r, double *rgb, int blocking);
  * Same return values as pt_render_step. */
 int pt_render_step_rgba8(pt_renderer *r, double *rgb, uint8_t *rgba, int blocking);
 /* Renderer::stop_rendering (mod.rs:55): the frame in flight is abandoned.  No
- * further band is queued, and the renderer's stop flag (host-mapped, read by
- * every launch of the frame as it starts) turns the launches already queued
- * into no-ops; the call returns once the device streams are idle, i.e. after
+ * further band is queued, and the renderer's stop flag (host-mapped, read at
+ * each sample chunk's start and after each compaction) turns the launches
+ * already queued into no-ops; the call returns once the device streams are
+ * idle, i.e. after
  * the kernels that were running when it was called (milliseconds, not the
  * seconds two whole bands take at 4K x 4096 spp).  Bands already copied by
  * render_step stay valid; the rest of the buffer is not written.  Frames

@@ -20,8 +20,8 @@ namespace dev {
 
 // A stop_rendering in flight (pt_render_stop): the frame is being discarded.
 // The flag is host-mapped memory, so a read crosses the host link (about a
-// microsecond): one thread per launch reads it (cp_scan, chunk_init) or one
-// per block (render_tiles), never one per wave of a hot kernel.
+// microsecond): one lane per launch reads it (stop_gate) or one per block
+// (render_tiles), never one per wave of a hot kernel.
 __device__ __forceinline__ bool stopped(const int *flag) {
     return flag && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }

@@ -147,7 +147,8 @@ struct WfView {
     // 64 B each (o, d, start, end); null when the march kernel selects itself
     double2 *jo;
     // per iteration: [0] the bounce's input count, [1] march-queue count,
-    // [2] long-march jobs, [3] set once the frame is being stopped
+    // [2] long-march jobs, [3] unused; word 3 (iteration 0) is the chunk's
+    // stop mark (stop_gate): set, the first bounce and wf_reduce do nothing
     uint32_t *cnt;
     double *acc;    // running per-pixel sums (3 per pixel of the tile group)
     uint32_t cap;   // path slots
@@ -289,7 +290,7 @@ template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_AN
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
-    const uint32_t count = v.cnt[it * 4 + 0];  // iteration 0: chunk_init's path count
+    const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
 #ifdef PT_BOUNCE_LANES
@@ -462,7 +463,7 @@ template <bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParams P, WfView v, int it,
                                                        uint32_t slice) {
     __shared__ uint32_t head;
-    const uint32_t count = v.cnt[it * 4 + 0];
+    const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
     const uint32_t G = gridDim.x;
     const uint32_t runs = (count + slice - 1) / slice;
     const uint32_t per = (runs > blockIdx.x ? (runs - blockIdx.x + G - 1) / G : 0u) * slice;
@@ -652,14 +653,9 @@ __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, 
 // tiles.  Runs longer than SCAN_RUN (more than 8192 tiles: chunks over 33M
 // paths) take the loop.
 constexpr int SCAN_RUN = 32;
-// A stop (the renderer's flag, read by thread 0 while the block scans) zeroes
-// the counts instead: the rest of the chunk's launches find no work, and
-// `mark` tells wf_reduce to skip the chunk.
 __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, uint32_t *__restrict__ n_live,
-                                               uint32_t *__restrict__ n_march, uint32_t *__restrict__ n_long,
-                                               const int *stop, uint32_t *__restrict__ mark) {
+                                               uint32_t *__restrict__ n_march, uint32_t *__restrict__ n_long) {
     __shared__ uint32_t lds[12];
-    const bool halt = threadIdx.x == 0 && dev::stopped(stop);
     const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
     const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
     uint32_t sl = 0, sg = 0, ss = 0, tl, tg, ts;
@@ -708,21 +704,21 @@ __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint3
         }
     }
     if (threadIdx.x == 0) {
-        *n_live = halt ? 0u : tl;
-        *n_march = halt ? 0u : tg + ts;
-        *n_long = halt ? 0u : tg;
-        *mark = halt ? 1u : 0u;
+        *n_live = tl;
+        *n_march = tg + ts;
+        *n_long = tg;
     }
 }
 
-// Chunk start: the chunk's counters cleared and iteration 0's input count set
-// (every path slot), or left at zero with the stop mark when the frame is
-// being stopped.
-__global__ __launch_bounds__(64) void chunk_init(uint32_t *__restrict__ cnt, uint32_t words, uint32_t paths,
-                                                 const int *stop) {
-    const bool halt = dev::stopped(stop);  // one request for the wave
-    for (uint32_t k = threadIdx.x; k < words; k += blockDim.x)
-        cnt[k] = k == 0 ? (halt ? 0u : paths) : k == 3 ? (halt ? 1u : 0u) : 0u;
+// Progressive frames only (FrameParams::stop set): at a chunk's start (it < 0)
+// and after each compaction, one lane reads the renderer's host-mapped stop
+// flag; set, the chunk's stop mark goes up and the compaction's counts go to
+// zero, so the chunk's remaining launches find no work.  One host-link read
+// per launch, not one per wave of the hot kernels.
+__global__ __launch_bounds__(64) void stop_gate(const int *stop, uint32_t *__restrict__ cnt, int it) {
+    if (threadIdx.x != 0 || !dev::stopped(stop)) return;
+    cnt[3] = 1u;
+    if (it >= 0) cnt[(it + 1) * 4 + 0] = cnt[it * 4 + 1] = cnt[it * 4 + 2] = 0u;
 }
 
 // The tile's ids are compacted into LDS first (in order), then copied out
@@ -1002,9 +998,9 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
 // registers and measured slower (the kernel is latency-bound: occupancy wins).
 template <bool EXT>
 __global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, WfView v, int first, int last,
-                                                 const uint32_t *__restrict__ mark, double *__restrict__ out) {
+                                                 double *__restrict__ out) {
     const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pl >= v.npix || *mark) return;  // a stopped frame's chunk: nothing to sum
+    if (pl >= v.npix || v.cnt[3]) return;  // v.cnt[3]: a stopped frame's chunk, nothing to sum
     uint32_t x, y, sl, pl2;
     slot_pixel(P, v, pl, &x, &y, &sl, &pl2);
     const uint32_t ti = v.tile0 + pl / (TILE * TILE), th = pl % (TILE * TILE);
@@ -1390,8 +1386,12 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             v.s0 = ch.s0;
             v.ns = ch.ns;
             const uint32_t paths = v.ns * v.npix;
-            chunk_init<<<1, 64, 0, cs>>>(v.cnt, (uint32_t)cnt_words, paths, P0.stop);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
+            (void)paths;  // (every bounce writes the status of each of its inputs; compaction reads no further)
+            if ((e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
+            if (P0.stop) {
+                stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, -1);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
         }
         for (int it = 0; it < iters; it++) {
             for (int j = 0; j < nr; j++) {
@@ -1426,8 +1426,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 const uint32_t *n_in = it == 0 ? nullptr : &v.cnt[it * 4 + 0];  // the bounce's input count
                 cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, n_in, paths);
                 cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
-                                                &v.cnt[it * 4 + 2], P0.stop, &v.cnt[(it + 1) * 4 + 3]);
+                                                &v.cnt[it * 4 + 2]);
                 cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq, n_in, paths);
+                if (P0.stop) stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, it);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (sc.nmarch == 0) continue;  // no ray-marched shape: the march queue is always empty
@@ -1457,11 +1458,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             const uint32_t s0 = v.s0;
             if (slots > 1 && r0 + j > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
-            const uint32_t *mark = &v.cnt[(iters - 1) * 4 + 3];  // the chunk's last compaction (or chunk_init)
             if (sc.ext)
-                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, mark, out);
+                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             else
-                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, mark, out);
+                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;

@@ -629,8 +629,23 @@ __device__ __forceinline__ uint4 cp_load(const uint8_t *__restrict__ st, const u
     return q;
 }
 
-// per tile: (live, long march, short march) counts in blk[3 * tile ..]
-__global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk,
+// Tile counts live in three arrays (live, long march, short march) of
+// per * 256 words, tile b at (b % per) * 256 + b / per with per =
+// ceil(tiles / 256): cp_scan's thread t owns tiles t * per .. t * per + per - 1,
+// and with this order a wave's loads of its threads' j-th tiles are 64
+// consecutive words.  (Tile-major, each load touched 64 lines: the scan took
+// 49 us per launch at 48M-path chunks, 12k tiles.)
+struct CpLayout {
+    uint32_t per, stride;  // tiles per scan thread, words per class array (per * 256)
+    __host__ __device__ static CpLayout of(uint32_t tiles) {
+        const uint32_t per = (tiles + CP_BLOCK - 1) / CP_BLOCK;
+        return CpLayout{per ? per : 1u, (per ? per : 1u) * CP_BLOCK};
+    }
+    __device__ uint32_t at(uint32_t b) const { return (b % per) * CP_BLOCK + b / per; }
+};
+
+// per tile: (live, long march, short march) counts
+__global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk, CpLayout L,
                                                 const uint32_t *__restrict__ n_dev, uint32_t n_host) {
     __shared__ uint32_t lds[12];
     const uint4 q = cp_load(st, n_dev, n_host);
@@ -640,45 +655,46 @@ __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, 
     block_exscan(g, &tg, lds + 4);
     block_exscan(m - g, &ts, lds + 8);
     if (threadIdx.x == 0) {
-        blk[3 * blockIdx.x] = tl;
-        blk[3 * blockIdx.x + 1] = tg;
-        blk[3 * blockIdx.x + 2] = ts;
+        const uint32_t k = L.at(blockIdx.x);
+        blk[k] = tl;
+        blk[L.stride + k] = tg;
+        blk[2 * L.stride + k] = ts;
     }
 }
 
 // one block: exclusive scan of the tile counts in place; totals go to the
 // counters the next kernels read (n_long: where the short march jobs start).
-// Each thread owns a contiguous run of tiles, loaded into registers up front
-// (every load in flight together), and the block scans once, not once per 256
-// tiles.  Runs longer than SCAN_RUN (more than 8192 tiles: chunks over 33M
-// paths) take the loop.
-constexpr int SCAN_RUN = 32;
-__global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, uint32_t *__restrict__ n_live,
-                                               uint32_t *__restrict__ n_march, uint32_t *__restrict__ n_long) {
+// Each thread owns a contiguous run of `per` tiles (CpLayout: coalesced across
+// the wave), loaded into registers up front (every load in flight together)
+// when the run is at most SCAN_RUN tiles, and the block scans once.
+constexpr int SCAN_RUN = 48;
+__global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, CpLayout L,
+                                               uint32_t *__restrict__ n_live, uint32_t *__restrict__ n_march,
+                                               uint32_t *__restrict__ n_long) {
     __shared__ uint32_t lds[12];
-    const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
-    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    const uint32_t per = L.per;
+    const uint32_t b0 = threadIdx.x * per;
+    const uint32_t nj = b0 >= nblk ? 0u : (nblk - b0 < per ? nblk - b0 : per);  // this thread's tiles
+    uint32_t *bl = blk + threadIdx.x, *bg = bl + L.stride, *bs = bg + L.stride;  // tile j at [j * 256]
     uint32_t sl = 0, sg = 0, ss = 0, tl, tg, ts;
     if (per <= (uint32_t)SCAN_RUN) {  // (block-uniform)
         uint32_t rl[SCAN_RUN], rg[SCAN_RUN], rs[SCAN_RUN];
 #pragma unroll
         for (int j = 0; j < SCAN_RUN; j++) {
-            const uint32_t b = b0 + j;
-            const bool ok = b < b1;
-            rl[j] = ok ? blk[3 * b] : 0u;
-            rg[j] = ok ? blk[3 * b + 1] : 0u;
-            rs[j] = ok ? blk[3 * b + 2] : 0u;
+            const bool ok = (uint32_t)j < nj;
+            rl[j] = ok ? bl[j * CP_BLOCK] : 0u;
+            rg[j] = ok ? bg[j * CP_BLOCK] : 0u;
+            rs[j] = ok ? bs[j * CP_BLOCK] : 0u;
         }
 #pragma unroll
         for (int j = 0; j < SCAN_RUN; j++) sl += rl[j], sg += rg[j], ss += rs[j];
         uint32_t cl = block_exscan(sl, &tl, lds), cg = block_exscan(sg, &tg, lds + 4), cs = block_exscan(ss, &ts, lds + 8);
 #pragma unroll
         for (int j = 0; j < SCAN_RUN; j++) {
-            const uint32_t b = b0 + j;
-            if (b < b1) {
-                blk[3 * b] = cl;
-                blk[3 * b + 1] = cg;
-                blk[3 * b + 2] = cs;
+            if ((uint32_t)j < nj) {
+                bl[j * CP_BLOCK] = cl;
+                bg[j * CP_BLOCK] = cg;
+                bs[j * CP_BLOCK] = cs;
             }
             cl += rl[j];
             cg += rg[j];
@@ -686,18 +702,18 @@ __global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint3
         }
     } else {
 #pragma unroll 8
-        for (uint32_t b = b0; b < b1; b++) {
-            sl += blk[3 * b];
-            sg += blk[3 * b + 1];
-            ss += blk[3 * b + 2];
+        for (uint32_t j = 0; j < nj; j++) {
+            sl += bl[j * CP_BLOCK];
+            sg += bg[j * CP_BLOCK];
+            ss += bs[j * CP_BLOCK];
         }
         uint32_t cl = block_exscan(sl, &tl, lds), cg = block_exscan(sg, &tg, lds + 4), cs = block_exscan(ss, &ts, lds + 8);
 #pragma unroll 8
-        for (uint32_t b = b0; b < b1; b++) {
-            const uint32_t l = blk[3 * b], g = blk[3 * b + 1], h = blk[3 * b + 2];
-            blk[3 * b] = cl;
-            blk[3 * b + 1] = cg;
-            blk[3 * b + 2] = cs;
+        for (uint32_t j = 0; j < nj; j++) {
+            const uint32_t l = bl[j * CP_BLOCK], g = bg[j * CP_BLOCK], h = bs[j * CP_BLOCK];
+            bl[j * CP_BLOCK] = cl;
+            bg[j * CP_BLOCK] = cg;
+            bs[j * CP_BLOCK] = cs;
             cl += l;
             cg += g;
             cs += h;
@@ -725,7 +741,7 @@ __global__ __launch_bounds__(64) void stop_gate(const int *stop, uint32_t *__res
 // with consecutive lanes on consecutive positions (one thread's 16 statuses
 // scattered straight to HBM would touch 64 lines per wave store).
 __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st, const uint32_t *__restrict__ blk,
-                                                  const uint32_t *__restrict__ n_long, uint32_t *__restrict__ live_out,
+                                                  CpLayout L, const uint32_t *__restrict__ n_long, uint32_t *__restrict__ live_out,
                                                   uint32_t *__restrict__ march_out, const uint32_t *__restrict__ n_dev,
                                                   uint32_t n_host) {
     __shared__ uint32_t lds[12];
@@ -742,7 +758,8 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
     for (int k = 0; k < CP_ITEMS; k++)
         if ((w[k >> 2] >> (8 * (k & 3))) & 1u) ids[ol++] = (uint32_t)(base + k);
     __syncthreads();
-    const uint32_t bl = blk[3 * blockIdx.x], bg = blk[3 * blockIdx.x + 1], bs = *n_long + blk[3 * blockIdx.x + 2];
+    const uint32_t kb = L.at(blockIdx.x);
+    const uint32_t bl = blk[kb], bg = blk[L.stride + kb], bs = *n_long + blk[2 * L.stride + kb];
     for (uint32_t k = threadIdx.x; k < tl; k += CP_BLOCK) live_out[bl + k] = ids[k];
     if (tg + ts == 0) return;  // (block-uniform)
     __syncthreads();
@@ -1290,7 +1307,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 8) * 3 +
                               (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 3 +
                               al((size_t)cap * 4 * (P0.depth + 1)) +
-                              al((size_t)cap_tiles * CP_TILE) + al((size_t)cap_tiles * 12) + al(cnt_words * 4) +
+                              al((size_t)cap_tiles * CP_TILE) + al(((size_t)cap_tiles + CP_BLOCK) * 12) + al(cnt_words * 4) +
                               al(att_bytes);
     const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
     e = reserve(ws, bytes);
@@ -1318,7 +1335,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         v.list = (uint32_t *)take((size_t)cap * 4);
         v.mq = (uint32_t *)take((size_t)cap * 4);
         v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
-        sl[k].cp_blk = (uint32_t *)take((size_t)cap_tiles * 12);
+        sl[k].cp_blk = (uint32_t *)take(((size_t)cap_tiles + CP_BLOCK) * 12);  // CpLayout: 3 x per * 256 words
         v.cnt = (uint32_t *)take(cnt_words * 4);
         v.att = att_bytes ? (double *)take(att_bytes) : nullptr;
         v.jo = presel ? (double2 *)take((size_t)cap * 64) : nullptr;
@@ -1424,10 +1441,12 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
                 const uint32_t *n_in = it == 0 ? nullptr : &v.cnt[it * 4 + 0];  // the bounce's input count
-                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, n_in, paths);
-                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
+                const CpLayout L = CpLayout::of(ptiles);
+                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, n_in, paths);
+                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, L, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
                                                 &v.cnt[it * 4 + 2]);
-                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, &v.cnt[it * 4 + 2], v.list, v.mq, n_in, paths);
+                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, &v.cnt[it * 4 + 2], v.list, v.mq, n_in,
+                                                        paths);
                 if (P0.stop) stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, it);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;

@@ -277,12 +277,6 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // points along a march job's chord whose sign of f predicts a hit (queue
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
 constexpr int WF_PREDICT = 4;
-#ifndef PT_BOUNCE_PRIO
-#define PT_BOUNCE_PRIO 0
-#endif
-#ifndef PT_MARCH_PRIO
-#define PT_MARCH_PRIO 0
-#endif
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
 #endif
@@ -295,9 +289,6 @@ constexpr int WF_PREDICT = 4;
 template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
-#if PT_BOUNCE_PRIO
-    __builtin_amdgcn_s_setprio(PT_BOUNCE_PRIO);
-#endif
     // input: the id-sorted list of live paths (iteration 0: every slot)
     const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -816,9 +807,6 @@ template <bool DIAG, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag,
                                                                             uint32_t slice) {
     __shared__ uint32_t head;
-#if PT_MARCH_PRIO
-    __builtin_amdgcn_s_setprio(PT_MARCH_PRIO);
-#endif
     const int nm = sc.nmarch;
     const uint32_t count = v.cnt[it * 4 + 1];
     const uint32_t *mq = v.mq;

@@ -317,13 +317,25 @@ PT_HD bool slab(const double *lo, const double *hi, const Ray &r, V3 inv, double
 // in the shape list — the linear scan's "later shape wins a tie" rule, which
 // makes the visiting order (uniform list, BVH, marched shapes last) irrelevant.
 // This part covers the uniform list and the BVH; marched shapes follow.
+// any: only whether the ray hits something matters (its hit will be shaded
+// at depth 0, where ray_color returns black for every hit, mod.rs:25-27):
+// the wave leaves the uniform list once each of its lanes has a hit, and a
+// lane with a hit skips the BVH.
+PT_HD bool wave_all(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __all(p);
+#else
+    return p;
+#endif
+}
 template <bool STATS = false, bool EXT = false>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
-                           Ctr *ct = nullptr) {
+                           Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
     int who = *who_out;
     // wave-uniform list (few JSON shapes): scalar loads of each shape
     for (int k = 0; k < sc.nlin; k++) {
+        if (any && wave_all(who >= 0)) break;
         const int i = uniform_load(&sc.lin[k]);
         const DShape s = uniform_shape(&sc.shapes[i]);
         if (s.type == CUBE || s.type == SPHERE) {
@@ -344,7 +356,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // ray's direction octant (near child first, pt_accel.hpp)
     const DNodeC *nodes = sc.nodes + (size_t)((r.d.x < 0.0 ? 1 : 0) | (r.d.y < 0.0 ? 2 : 0) | (r.d.z < 0.0 ? 4 : 0)) *
                                         (size_t)sc.nnodes;
-    int n = 0;
+    int n = any && who >= 0 ? sc.nnodes : 0;
     while (n < sc.nnodes) {
         const DNodeC nd = nodes[n];
         if (STATS) ct->c[C_NODE_SLABS]++;

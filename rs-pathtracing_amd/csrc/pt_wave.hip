@@ -389,11 +389,15 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             best = __builtin_inf();
             who = -1;
-            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
+            // the hit of this trace is shaded at depth `depth`: at 0 only hit or
+            // miss matters (any hit gives black), so a path with a hit found
+            // needs no march either
+            const bool any = depth == 0;
+            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
             // march kernel marches it)
-            for (int k = 0; k < sc.nmarch && !need_march; k++) {
+            for (int k = 0; k < sc.nmarch && !need_march && !(any && who >= 0); k++) {
                 const int s = dev::uniform_load(&sc.march[k]);
                 const DBox bx = dev::uniform_box(&sc.boxes[s]);
                 if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
@@ -427,6 +431,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 }
             }
             PT_BSTAMP(5)
+            if (any && !need_march) {
+                // its shade would end it at once (mod.rs:24-27, 42-44): black
+                // after a hit, the background after a miss; only paths whose
+                // answer needs a march go on to the last iteration
+                end_path(v, id, stk, who >= 0 ? dev::v3(0.0, 0.0, 0.0) : dev::background(ray.d));
+                live = false;
+            }
         }
         // every input position's state is written (ended paths too: whole lines; storeab)
         if (i < count)

@@ -21,10 +21,12 @@ declare -A SAMPLES=([c2]=530841600 [c3]=8493465600 [c5]=530841600)
 declare -A WL=([c2]="cornell_box.json 1920x1080 256spp depth 8" [c3]="cornell_box.json 3840x2160 1024spp depth 8"
                [c5]="synthetic_100000 1920x1080 256spp depth 8")
 if [ "$what" = pmc ] || [ "$what" = all ]; then
-    for c in c2 c3 c5; do
-        WORKLOAD="${WL[$c]}" SQ_FRAMES=1 SQ_SAMPLES=${SAMPLES[$c]} PROF_TIMEOUT=300 \
+    for c in ${PMC_CONFIGS:-c2 c5 c3}; do
+        # c3 (~4,000 dispatches per frame): counters on the render kernels only (unfiltered, rocprofv3 crashed)
+        F=""; if [ $c = c3 ]; then F="wf_bounce|wf_march"; fi
+        PMC_FILTER="$F" WORKLOAD="${WL[$c]}" SQ_FRAMES=1 SQ_SAMPLES=${SAMPLES[$c]} PROF_TIMEOUT=300 \
             bash scripts/gpu.sh sq $tag/pmc_$c --config $c $ONE
-        WORKLOAD="${WL[$c]}" PROF_TIMEOUT=300 bash scripts/gpu.sh pmc $tag/pmc_$c --config $c $ONE
+        PMC_FILTER="$F" WORKLOAD="${WL[$c]}" PROF_TIMEOUT=300 bash scripts/gpu.sh pmc $tag/pmc_$c --config $c $ONE
         echo "pmc $c done" >> $OUT/progress.txt
     done
 fi

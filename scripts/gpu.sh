@@ -19,6 +19,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$tag
 mkdir -p $OUT
 cd $R
+# PMC_FILTER (optional): a kernel-name regex; counter passes collect only those kernels' dispatches
+# (the c3 frame's ~4,000 dispatches crashed rocprofv3's counter collection in round 3 without it)
+FILT=(); if [ -n "$PMC_FILTER" ]; then FILT=(--kernel-include-regex "$PMC_FILTER"); fi
 prof() {  # rocprofv3 with the program itself after -- (no launcher hops)
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL ${PROF_TIMEOUT:-400} rocprofv3 "$@")
 }
@@ -37,14 +40,14 @@ kt)
     python3 scripts/kt_summary.py $OUT/kt > $OUT/kt_summary.txt
     python3 scripts/kt_leg.py $OUT/kt/bench_kernel_trace.csv $(( ${KT_FRAMES:-5} )) > $OUT/kt_one_stream_frame.txt || true ;;
 pmc)
-    prof --kernel-trace --output-format csv -d $OUT/fetch -o p --pmc FETCH_SIZE -- python3 $R/bench.py "$@" \
+    prof --kernel-trace --output-format csv -d $OUT/fetch -o p "${FILT[@]}" --pmc FETCH_SIZE -- python3 $R/bench.py "$@" \
         > $OUT/fetch.log 2>&1
-    prof --kernel-trace --output-format csv -d $OUT/write -o p --pmc WRITE_SIZE -- python3 $R/bench.py "$@" \
+    prof --kernel-trace --output-format csv -d $OUT/write -o p "${FILT[@]}" --pmc WRITE_SIZE -- python3 $R/bench.py "$@" \
         > $OUT/write.log 2>&1
     python3 scripts/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json "${WORKLOAD:-cornell_box.json 1920x1080 256spp depth 8}" \
         > $OUT/traffic.log ;;
 sq)
-    prof --kernel-trace --output-format csv -d $OUT/sq -o p --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
+    prof --kernel-trace --output-format csv -d $OUT/sq -o p "${FILT[@]}" --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
         SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVES \
         -- python3 $R/bench.py "$@" > $OUT/sq.log 2>&1
     python3 scripts/pmc_summary.py $OUT/sq > $OUT/sq_summary.txt

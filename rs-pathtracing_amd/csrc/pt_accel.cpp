@@ -184,7 +184,10 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
         for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());
     }
     a.cnodes.reserve(a.nodes.size());
-    for (const DNode &n : a.nodes) {
+    const size_t per_oct = a.nodes.size() / BVH_OCTANTS;
+    for (size_t ni = 0; ni < a.nodes.size(); ni++) {
+        const DNode &n = a.nodes[ni];
+        const int oct = per_oct ? (int)(ni / per_oct) : 0;
         if (n.first < 0 || n.first >= (1 << 24) || n.count < 0 || n.count > 255)
             throw std::runtime_error("BVH too large for the compact node form (leaf index >= 2^24)");
         DNodeC c{};
@@ -192,8 +195,9 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
             float lo = (float)n.lo[k], hi = (float)n.hi[k];
             if ((double)lo > n.lo[k]) lo = std::nextafter(lo, -INFINITY);
             if ((double)hi < n.hi[k]) hi = std::nextafter(hi, INFINITY);
-            c.lo[k] = lo;
-            c.hi[k] = hi;
+            const bool neg = (oct >> k) & 1;  // the octant's rays move toward -k: hi is the near plane
+            c.nr[k] = neg ? hi : lo;
+            c.fr[k] = neg ? lo : hi;
         }
         c.skip = n.skip;
         // a one-shape leaf holds the shape id itself (bit 31), saving the dependent leaf[] load

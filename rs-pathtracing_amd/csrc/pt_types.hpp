@@ -68,8 +68,11 @@ static_assert(sizeof(DNode) == 64, "DNode is one cache line");
 // first | count << 24 (leaves hold at most 16 shapes; first < 2^24 is checked
 // when the BVH is built); bit 31 marks a one-shape leaf whose `first` is the
 // shape id itself rather than an index into the leaf list.
+// In octant o's layout (pt_accel.hpp) the box is stored as near and far
+// planes: for an axis where o's ray direction is negative (sign bit set) the
+// two are the box's hi and lo, so the walk needs no min/max per axis.
 struct alignas(32) DNodeC {
-    float lo[3], hi[3];
+    float nr[3], fr[3];
     int32_t skip;
     uint32_t first_count;
 };

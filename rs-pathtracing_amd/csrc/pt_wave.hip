@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             // does any marched shape's bound start before the best hit? (the
             // march kernel marches it)
             for (int k = 0; k < sc.nmarch && !need_march && !(any && who >= 0); k++) {
-                const int s = dev::uniform_load(&sc.march[k]);
+                const int s = dev::uniform_index(dev::uniform_load(&sc.march[k]));
                 const DBox bx = dev::uniform_box(&sc.boxes[s]);
                 if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
                 const DShape S = dev::uniform_shape(&sc.shapes[s]);

@@ -70,7 +70,13 @@ extern "C" int h_node_check(void *p) {
     int bad = 0;
     for (size_t i = 0; i < N.size(); i++) {
         bool ok = Cn[i].skip == N[i].skip;
-        for (int k = 0; k < 3; k++) ok = ok && (double)Cn[i].lo[k] <= N[i].lo[k] && (double)Cn[i].hi[k] >= N[i].hi[k];
+        const size_t per = N.size() / BVH_OCTANTS;
+        const int oct = per ? (int)(i / per) : 0;  // layout oct stores (near, far) planes: (hi, lo) on its negative axes
+        for (int k = 0; k < 3; k++) {
+            const bool neg = (oct >> k) & 1;
+            const double lo = neg ? Cn[i].fr[k] : Cn[i].nr[k], hi = neg ? Cn[i].nr[k] : Cn[i].fr[k];
+            ok = ok && lo <= N[i].lo[k] && hi >= N[i].hi[k];
+        }
         const uint32_t fc = Cn[i].first_count;
         const int count = (int)(fc >> 24 & 0x7fu), first = (int)(fc & 0xffffffu);
         ok = ok && count == N[i].count;

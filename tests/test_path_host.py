@@ -184,3 +184,42 @@ def test_synthetic_field_ground_sphere_uniform_and_octant_bvh(H):
     H.h_trace_pixels(pr.h, w, h, 2, 8, 3, px.ctypes.data_as(C.POINTER(C.c_uint32)), len(px),
                      out.ctypes.data_as(C.POINTER(C.c_double)))
     assert np.array_equal(out, pr.o.render(w, h, 2, 8, 3, pixels=px))
+
+
+def test_bvh_walk_signed_zero_and_axis_rays(H):
+    """The BVH stores each octant's boxes as near/far planes picked by the
+    direction's sign bits and intersects them with t = fma(b, 1/d, -o/d): rays
+    with +0 / -0 components (1/d = +-inf, NaN t's), axis-parallel rays and
+    origins on the spheres' bounding planes must still find the oracle's
+    closest hit (the cull has to stay conservative)."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    pr = Pair(H, json.dumps(make_scenes.synthetic(400)), seed=1)
+    rng = np.random.default_rng(11)
+    spheres = [s for s in make_scenes.synthetic(400)["shapes"][1:]]
+    rays = []
+    for _ in range(600):
+        c = np.array(spheres[rng.integers(len(spheres))]["transform"]["translate"], float)
+        # (not tangent to a sphere: a ray with disc == 0 takes the reference's unranged root, whose winner
+        # depends on the visiting order, DESIGN.md §7)
+        o = c + rng.choice([-0.2000001, 0.2000001, 0.1, 0.0], size=3) + rng.choice([0.0, 0.5, -0.5], size=3)
+        o[1] = max(o[1], 0.05)
+        d = np.zeros(3)
+        k = rng.integers(3)
+        d[k] = rng.choice([-1.0, 1.0])
+        for j in range(3):
+            if j != k:
+                d[j] = rng.choice([0.0, -0.0, 1e-300, -1e-300, rng.normal() * 0.3])
+        d /= np.linalg.norm(d)
+        rays.append(np.concatenate([o, d]))
+    hits = 0
+    for ray in rays:
+        who, t, p, n, f = pr.closest(ray)
+        h = pr.o.closest_hit(ray[:3], ray[3:])
+        if h is None:
+            assert who == -1, ray
+        else:
+            hits += 1
+            assert (who, t, p, n, f) == (h.shape, h.t, list(h.point), list(h.normal), h.front_face), ray
+    assert hits > 100

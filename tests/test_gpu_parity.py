@@ -446,3 +446,45 @@ def test_textured_probes_and_shards(pt, monkeypatch):
     assert np.array_equal(frame.view(-1, 3).cpu().numpy(), full)
     cnt = pt.count_work(r, cam, pt.ImageParams(w, h), 2, pixels, seed=1)
     assert cnt["samples"] == 2 * len(pixels)
+
+
+def test_bvh_signed_zero_and_axis_rays_on_device(pt):
+    """The device BVH walk (near/far planes per octant layout, octant from the direction's sign bits) on rays
+    with +0 / -0 / denormal components and origins around the spheres' bounding planes: the GPU's closest hits
+    equal the oracle's linear scan (the host build runs the same rays in tests/test_path_host.py)."""
+    import json
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    scene = make_scenes.synthetic(400)
+    text = json.dumps(scene)
+    ps, osc = pt.Scene.from_json(text, seed=1), O.Scene(text, seed=1)
+    r = pt.HipRenderer(ps, depth=8)
+    rng = np.random.default_rng(11)
+    centres = [np.array(s["transform"]["translate"], float) for s in scene["shapes"][1:]]
+    rays = []
+    for _ in range(2000):
+        o = centres[rng.integers(len(centres))] + rng.choice([-0.2000001, 0.2000001, 0.1, 0.0], size=3) \
+            + rng.choice([0.0, 0.5, -0.5], size=3)
+        o[1] = max(o[1], 0.05)
+        d = np.zeros(3)
+        k = rng.integers(3)
+        d[k] = rng.choice([-1.0, 1.0])
+        for j in range(3):
+            if j != k:
+                d[j] = rng.choice([0.0, -0.0, 1e-300, -1e-300, rng.normal() * 0.3])
+        d /= np.linalg.norm(d)
+        rays.append(np.concatenate([o, d]))
+    rays = np.array(rays)
+    got = r.closest_hit(rays)
+    hits = 0
+    for i, ray in enumerate(rays):
+        h = osc.closest_hit(ray[:3], ray[3:])
+        g = got[i]
+        if h is None:
+            assert g["shape"] == -1, ray
+            continue
+        hits += 1
+        assert (g["shape"], g["t"], list(g["point"])) == (h.shape, h.t, list(h.point)), ray
+    assert hits > 300

@@ -340,7 +340,7 @@ PT_HD bool wave_all(bool p) {
     return p;
 #endif
 }
-template <bool STATS = false, bool EXT = false>
+template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
                            Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
@@ -371,20 +371,28 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // planes for that octant, so a node's entry and exit are max(near t's,
     // min_t) and min(far t's, best): 6 min/max instead of 12 (C5 +2.2 %).  The
     // t's round as the symmetric slab's do; a NaN t (1/d infinite and b = o)
-    // drops out of fmax/fmin and leaves that axis open (conservative).  The
-    // form t = fma(b, 1/d, -o/d) was faster on C5 (+3.9 %) but its three live
-    // -o/d values cost the C2 bounce kernel's register allocation 9 %.
+    // drops out of fmax/fmin and leaves that axis open (conservative).
+    // FMA_SLAB (the wavefront builds for scenes with a large BVH, C5): t =
+    // fma(b, 1/d, -o/d), 6 FMAs instead of 6 subtractions and 6 multiplies
+    // (C5 +1.7 %); its rounding moves a plane by ~2^-53 (|b| + |o|) as the
+    // subtraction's does, far inside the boxes' padding, and an infinite 1/d
+    // gives NaN t's (an open axis, conservative).  Not in the other builds:
+    // its three live -o/d values cost the C2 bounce kernel 9 % through
+    // register allocation (profiles/r3/ab_round3_experiments.txt r3y).
     const int oct = (__builtin_signbit(r.d.x) ? 1 : 0) | (__builtin_signbit(r.d.y) ? 2 : 0) |
                     (__builtin_signbit(r.d.z) ? 4 : 0);
     const DNodeC *nodes = sc.nodes + (size_t)oct * (size_t)sc.nnodes;
+    const double mx = FMA_SLAB ? -(r.o.x * inv.x) : 0.0, my = FMA_SLAB ? -(r.o.y * inv.y) : 0.0,
+                 mz = FMA_SLAB ? -(r.o.z * inv.z) : 0.0;
+    auto tx = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.x, mx) : ((double)b - r.o.x) * inv.x; };
+    auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
+    auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };
     int n = any && who >= 0 ? sc.nnodes : 0;
     while (n < sc.nnodes) {
         const DNodeC nd = nodes[n];
         if (STATS) ct->c[C_NODE_SLABS]++;
-        const double tn = fmax(fmax(((double)nd.nr[0] - r.o.x) * inv.x, ((double)nd.nr[1] - r.o.y) * inv.y),
-                               fmax(((double)nd.nr[2] - r.o.z) * inv.z, min_t));
-        const double tf = fmin(fmin(((double)nd.fr[0] - r.o.x) * inv.x, ((double)nd.fr[1] - r.o.y) * inv.y),
-                               fmin(((double)nd.fr[2] - r.o.z) * inv.z, best));
+        const double tn = fmax(fmax(tx(nd.nr[0]), ty(nd.nr[1])), fmax(tz(nd.nr[2]), min_t));
+        const double tf = fmin(fmin(tx(nd.fr[0]), ty(nd.fr[1])), fmin(tz(nd.fr[2]), best));
         if (tn <= tf) {
             const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24 & 0x7fu);
             const bool direct = nd.first_count >> 31;  // one-shape leaf: `first` is the shape id

@@ -286,7 +286,8 @@ constexpr int WF_PREDICT = 4;
 // full s_waitcnt so the memory waits it causes are charged to it (tuning
 // only): list load, state loads, shade, unwind, trace, march pre-check,
 // stores; summed into diag[36..42].
-template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false>
+template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false,
+          bool BIGBVH = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             // miss matters (any hit gives black), so a path with a hit found
             // needs no march either
             const bool any = depth == 0;
-            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+            dev::closest_nomarch<false, EXT, BIGBVH>(sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
             // march kernel marches it)
@@ -1154,6 +1155,9 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
     return hipSuccess;
 }
 
+// BVH nodes per octant layout from which the bounce runs its FMA_SLAB build
+// (dev::closest_nomarch): C5's 100k-sphere tree has ~200k, cornell's ~960.
+constexpr int BIG_BVH_NODES = 1 << 15;
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
                           const WfView &v, int it, unsigned long long *diag, int fkind, int waves) {
@@ -1171,6 +1175,10 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
     }
     if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
         wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        return;
+    }
+    if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH (C5): the FMA slab build
+        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves

@@ -165,3 +165,20 @@ extern "C" void h_count_work(void *p, uint32_t w, uint32_t h, uint32_t spp, uint
     }
     for (int k = 0; k < C_COUNT; k++) counters[k] = c.c[k];
 }
+
+// The non-marched closest hit (uniform list + BVH) with the BVH slab in one of
+// its two arithmetic forms: fma = 0 (b - o) * 1/d, 1 fma(b, 1/d, -o/d) (the
+// FMA_SLAB bounce build for large BVHs).  Both must give the same (who, t).
+extern "C" int h_closest_nomarch(void *p, const double *ray, int fma, double *t) {
+    Bundle *b = (Bundle *)p;
+    dev::Ray r;
+    r.o = dev::v3(ray[0], ray[1], ray[2]);
+    r.d = dev::v3(ray[3], ray[4], ray[5]);
+    const dev::V3 inv = dev::v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+    double best = __builtin_inf();
+    int who = -1;
+    if (fma) dev::closest_nomarch<false, false, true>(b->view, r, inv, T_MIN, &best, &who);
+    else dev::closest_nomarch<false, false, false>(b->view, r, inv, T_MIN, &best, &who);
+    *t = best;
+    return who;
+}

@@ -223,3 +223,36 @@ def test_bvh_walk_signed_zero_and_axis_rays(H):
             hits += 1
             assert (who, t, p, n, f) == (h.shape, h.t, list(h.point), list(h.normal), h.front_face), ray
     assert hits > 100
+
+
+def test_bvh_fma_slab_build_same_hits(H):
+    """The bounce build for large BVHs computes the node planes' t as fma(b, 1/d, -o/d) (FMA_SLAB); on the
+    synthetic field, with random and signed-zero / axis-parallel rays, it returns the same (shape, t) as the
+    subtract-multiply build (the culls differ only in rounding, far inside the boxes' padding)."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    H.h_closest_nomarch.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    scene = make_scenes.synthetic(3000)
+    pr = Pair(H, json.dumps(scene), seed=1)
+    rng = np.random.default_rng(17)
+    centres = [np.array(s["transform"]["translate"], float) for s in scene["shapes"][1:]]
+    hits = 0
+    for i in range(4000):
+        if i % 2:
+            o = rng.uniform([-15, 0.05, -15], [15, 3, 15])
+            d = rng.normal(size=3)
+        else:
+            o = centres[rng.integers(len(centres))] + rng.choice([-0.2000001, 0.2000001, 0.0], size=3)
+            o[1] = max(o[1], 0.05)
+            d = np.zeros(3)
+            d[rng.integers(3)] = rng.choice([-1.0, 1.0])
+            d = np.where(d == 0, rng.choice([0.0, -0.0, 1e-300, rng.normal() * 0.3], size=3), d)
+        d /= np.linalg.norm(d)
+        ray = (C.c_double * 6)(*np.concatenate([o, d]))
+        t0, t1 = C.c_double(), C.c_double()
+        w0 = H.h_closest_nomarch(pr.h, ray, 0, C.byref(t0))
+        w1 = H.h_closest_nomarch(pr.h, ray, 1, C.byref(t1))
+        assert (w0, t0.value) == (w1, t1.value), (o, d)
+        hits += w0 >= 0
+    assert hits > 1000

@@ -24,7 +24,9 @@ if [ "$what" = pmc ] || [ "$what" = all ]; then
     for c in ${PMC_CONFIGS:-c2 c5 c3}; do
         # c3 (~4,000 dispatches per frame): counters on the render kernels only (unfiltered, rocprofv3 crashed)
         F=""; if [ $c = c3 ]; then F="wf_bounce|wf_march"; fi
-        PMC_FILTER="$F" WORKLOAD="${WL[$c]}" SQ_FRAMES=1 SQ_SAMPLES=${SAMPLES[$c]} PROF_TIMEOUT=300 \
+        # c5 runs the FMA_SLAB bounce build: its FMAs beyond the expansions' 6.32 per TRANS are algorithmic
+        R=""; if [ $c = c5 ]; then R=6.32; fi
+        PMC_FMA_PER_TRANS="$R" PMC_FILTER="$F" WORKLOAD="${WL[$c]}" SQ_FRAMES=1 SQ_SAMPLES=${SAMPLES[$c]} PROF_TIMEOUT=300 \
             bash scripts/gpu.sh sq $tag/pmc_$c --config $c $ONE
         PMC_FILTER="$F" WORKLOAD="${WL[$c]}" PROF_TIMEOUT=300 bash scripts/gpu.sh pmc $tag/pmc_$c --config $c $ONE
         echo "pmc $c done" >> $OUT/progress.txt

@@ -235,6 +235,9 @@ def profile_file(name, workload, source):
 
 def main():
     args = parse()
+    if os.environ.get("PT_SEGV_LOG"):  # diagnostics: a host fault's address, registers and mappings to a file
+        import ctypes
+        ctypes.CDLL(str(ROOT / "tools" / "segv_maps.so")).pt_segv_install(os.environ["PT_SEGV_LOG"].encode())
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -69,19 +69,21 @@ typedef int (*pt_image_loader)(void *user, const char *filename, uint32_t *width
 /* The struct is versioned by struct_size, which the library honours: it reads
  * no byte at or past opts + struct_size.  A caller sets struct_size =
  * sizeof(pt_scene_opts) of the header it was compiled against (or uses
- * PT_SCENE_OPTS_INIT).  struct_size == 0 is a version-1 caller (0.2.0 and
- * earlier, this field was `reserved`, always 0): its struct is the 16 bytes
- * {random_spheres, reserved, seed} and load_image / image_user are never
- * read.  A size between 1 and 15 is rejected (PT_ERR_INVALID); fields a newer
+ * PT_SCENE_OPTS_INIT).  struct_size == 0 is a caller built against 0.1.0 or
+ * 0.2.0, where this field was `reserved` (always 0) and the struct already had
+ * this 32-byte layout: every field is read, load_image and image_user
+ * included.  A size between 1 and 15 is rejected (PT_ERR_INVALID); a size of
+ * 16 to 31 reads only the fields it covers (16: no loader); fields a newer
  * caller appends past sizeof(pt_scene_opts) are ignored. */
 typedef struct {
     uint32_t random_spheres; /* 1 = reference behaviour (default), 0 = JSON shapes only */
-    uint32_t struct_size;    /* sizeof(pt_scene_opts); 0 = version-1 16-byte struct */
+    uint32_t struct_size;    /* sizeof(pt_scene_opts); 0 = a 0.1.0 / 0.2.0 caller's struct of this layout */
     uint64_t seed; /* seed of the add_random_spheres stream and of the NoiseTexture Perlin tables */
     pt_image_loader load_image; /* NULL: built-in PPM reader (read only if struct_size covers it) */
     void *image_user;
 } pt_scene_opts;
-#define PT_SCENE_OPTS_V1_SIZE 16
+#define PT_SCENE_OPTS_MIN_SIZE 16    /* {random_spheres, struct_size, seed} */
+#define PT_SCENE_OPTS_LEGACY_SIZE 32 /* what struct_size == 0 means: the 0.1.0 / 0.2.0 struct */
 #define PT_SCENE_OPTS_INIT {1u, (uint32_t)sizeof(pt_scene_opts), 1u, NULL, NULL}
 
 /* Camera (src/camera/mod.rs:36-46).  fov in radians, as Camera::new takes it. */

@@ -181,10 +181,13 @@ int pt_scene_create_from_json(const char *json, size_t len, const pt_scene_opts 
     if (!json || !out) return fail(PT_ERR_INVALID, "null argument");
     *out = nullptr;
     // struct_size versions the options (header): no byte at or past
-    // opts + struct_size is read; 0 is a version-1 caller's 16-byte struct
-    const size_t osz = !opts ? 0 : (opts->struct_size ? opts->struct_size : (size_t)PT_SCENE_OPTS_V1_SIZE);
-    if (opts && osz < PT_SCENE_OPTS_V1_SIZE)
-        return fail(PT_ERR_INVALID, "pt_scene_opts.struct_size " + std::to_string(osz) + " is below the 16-byte version-1 struct");
+    // opts + struct_size is read; 0 is a 0.1.0 / 0.2.0 caller, whose struct
+    // (with `reserved` = 0 in this field) already had the 32-byte layout and
+    // its image loader
+    const size_t osz = !opts ? 0 : (opts->struct_size ? opts->struct_size : (size_t)PT_SCENE_OPTS_LEGACY_SIZE);
+    if (opts && osz < PT_SCENE_OPTS_MIN_SIZE)
+        return fail(PT_ERR_INVALID, "pt_scene_opts.struct_size " + std::to_string(osz) +
+                                        " is below the 16 bytes of {random_spheres, struct_size, seed}");
     bool rs = opts ? opts->random_spheres != 0 : true;
     uint64_t seed = opts ? opts->seed : 1;
     ImageSource img;
@@ -292,36 +295,76 @@ void free_share(GpuShare &g) {
     g.stream = nullptr;
 }
 
-// The acceleration structure on one device (replacing any previous one):
-// octant-threaded BVH nodes, leaf shape ids, the wave-uniform and marched
-// lists and the padded boxes.
-int upload_accel(GpuShare &g, const Accel &acc) {
-    HIP_TRY(hipSetDevice(g.device));
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    DeviceScene &d = g.ds;
-    void *old[] = {d.nodes, d.leaf, d.lin, d.march, d.boxes};
-    for (void *p : old)
-        if (p) HIP_TRY(hipFree(p));
-    d.nodes = nullptr;
-    d.leaf = d.lin = d.march = nullptr;
-    d.boxes = nullptr;
-    hipError_t err = hipSuccess;
+// The acceleration structure on one device: octant-threaded BVH nodes, leaf
+// shape ids, the wave-uniform and marched lists and the padded boxes.  A new
+// structure is first staged in buffers of its own (stage_accel); only when
+// every device has staged it are the old buffers swapped out and freed
+// (commit_accel), so a failed upload leaves every device on its old, complete
+// structure.
+struct StagedAccel {
+    DNodeC *nodes = nullptr;
+    int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
+    DBox *boxes = nullptr;
+    int nnodes = 0, nlin = 0, nmarch = 0;
+};
+
+// Test hook (renderer option "fault_accel_alloc" = n): the n-th device
+// allocation of the next BVH rebuild fails as if the device were out of memory.
+std::atomic<int> g_fault_accel_alloc{0};
+
+void free_staged(int device, StagedAccel &a) {
+    (void)hipSetDevice(device);
+    void *bufs[] = {a.nodes, a.leaf, a.lin, a.march, a.boxes};
+    for (void *p : bufs)
+        if (p) (void)hipFree(p);
+    a = StagedAccel{};
+}
+
+int stage_accel(int device, const Accel &acc, StagedAccel *out) {
+    StagedAccel a;
+    hipError_t err = hipSetDevice(device);
     auto upload = [&err](auto **dst, const auto &vec) {
         using T = typename std::remove_reference<decltype(vec)>::type::value_type;
         size_t n = vec.empty() ? 1 : vec.size();
+        if (err == hipSuccess && g_fault_accel_alloc.load() > 0 && g_fault_accel_alloc.fetch_sub(1) == 1)
+            err = hipErrorOutOfMemory;
         if (err == hipSuccess) err = hipMalloc((void **)dst, n * sizeof(T));
         if (err == hipSuccess && !vec.empty())
             err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice);
     };
-    upload(&d.nodes, acc.cnodes);
-    upload(&d.leaf, acc.leaf);
-    upload(&d.lin, acc.lin);
-    upload(&d.march, acc.march);
-    upload(&d.boxes, acc.boxes);
-    if (err != hipSuccess) return hip_fail(err, "uploading the acceleration structure");
-    d.nnodes = acc.nodes_per_octant();  // nodes per octant layout
-    d.nlin = (int)acc.lin.size();
-    d.nmarch = (int)acc.march.size();
+    upload(&a.nodes, acc.cnodes);
+    upload(&a.leaf, acc.leaf);
+    upload(&a.lin, acc.lin);
+    upload(&a.march, acc.march);
+    upload(&a.boxes, acc.boxes);
+    if (err != hipSuccess) {
+        free_staged(device, a);
+        return hip_fail(err, "uploading the acceleration structure");
+    }
+    a.nnodes = acc.nodes_per_octant();  // nodes per octant layout
+    a.nlin = (int)acc.lin.size();
+    a.nmarch = (int)acc.march.size();
+    *out = a;
+    return PT_OK;
+}
+
+// Swaps a staged structure in; the old one is freed once the device's queued
+// work (which may still read it) is done.
+int commit_accel(GpuShare &g, StagedAccel &a) {
+    HIP_TRY(hipSetDevice(g.device));
+    HIP_TRY(hipDeviceSynchronize());
+    DeviceScene &d = g.ds;
+    StagedAccel old{d.nodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch};
+    d.nodes = a.nodes;
+    d.leaf = a.leaf;
+    d.lin = a.lin;
+    d.march = a.march;
+    d.boxes = a.boxes;
+    d.nnodes = a.nnodes;
+    d.nlin = a.nlin;
+    d.nmarch = a.nmarch;
+    a = StagedAccel{};
+    free_staged(g.device, old);
     return PT_OK;
 }
 
@@ -350,7 +393,9 @@ int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const 
     if (err == hipSuccess) err = hipMalloc((void **)&g.ds.guard, sizeof(unsigned long long));
     if (err == hipSuccess) err = hipMemset(g.ds.guard, 0, sizeof(unsigned long long));
     if (err != hipSuccess) return hip_fail(err, "uploading the scene");
-    if (int rc = upload_accel(g, acc)) return rc;
+    StagedAccel a;
+    if (int rc = stage_accel(device, acc, &a)) return rc;
+    if (int rc = commit_accel(g, a)) return rc;
     g.ws.tune = tuning_from_env();
     g.ds.diag = g.ws.tune.diag;
     g.ds.nshapes = (int)hs.size();
@@ -525,11 +570,9 @@ int enable_peers(pt_renderer *r) {
         for (int way = 0; way < 2; way++) {
             HIP_TRY(hipSetDevice(way == 0 ? dk : d0));
             const hipError_t e = hipDeviceEnablePeerAccess(way == 0 ? d0 : dk, 0);
-            if (e == hipErrorPeerAccessAlreadyEnabled) {
-                (void)hipGetLastError();  // clear the sticky "already enabled"
-            } else if (e != hipSuccess) {
-                return hip_fail(e, "hipDeviceEnablePeerAccess");
-            }
+            // "already enabled" is success; any other error leaves this pair on the staged
+            // hipMemcpyPeerAsync (still correct): clear the error and carry on
+            if (e != hipSuccess) (void)hipGetLastError();
             ok = ok && (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled);
         }
         if (ok) r->peer_enabled++;
@@ -628,16 +671,32 @@ int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
         Tuning t = r->gpus[0].ws.tune;
         if (tuning_set(&t, name, value) != PT_OK)
             return fail(PT_ERR_INVALID, "bvh_leaf out of range (1..16): " + std::to_string((long long)value));
+        std::vector<StagedAccel> staged(r->gpus.size());
+        auto drop = [&] {
+            for (size_t k = 0; k < staged.size(); k++) free_staged(r->gpus[k].device, staged[k]);
+        };
         try {
             const Accel acc = build_accel(r->scene->s, r->scene->s.json_shapes, t.bvh_leaf);
-            for (auto &g : r->gpus) {
-                HIP_TRY(hipSetDevice(g.device));
-                HIP_TRY(hipDeviceSynchronize());
-                if (int rc = upload_accel(g, acc)) return rc;
-            }
+            // every device stages the new tree before any device lets go of the old one
+            for (size_t k = 0; k < r->gpus.size(); k++)
+                if (int rc = stage_accel(r->gpus[k].device, acc, &staged[k])) {
+                    drop();
+                    return rc;
+                }
         } catch (const std::exception &e) {
+            drop();
             return fail(PT_ERR_INVALID, std::string("rebuilding the BVH: ") + e.what());
         }
+        for (size_t k = 0; k < r->gpus.size(); k++)
+            if (int rc = commit_accel(r->gpus[k], staged[k])) {
+                drop();  // the devices before k run the new tree, k and after the old one: both complete
+                return rc;
+            }
+    }
+    if (!std::strcmp(name, "fault_accel_alloc")) {  // test hook, see g_fault_accel_alloc
+        if (value < 0 || value > 64) return fail(PT_ERR_INVALID, "fault_accel_alloc out of range (0..64)");
+        g_fault_accel_alloc.store((int)value);
+        return PT_OK;
     }
     for (auto &g : r->gpus) {
         Tuning t = g.ws.tune;

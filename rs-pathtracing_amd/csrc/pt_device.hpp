@@ -382,8 +382,12 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     const int oct = (__builtin_signbit(r.d.x) ? 1 : 0) | (__builtin_signbit(r.d.y) ? 2 : 0) |
                     (__builtin_signbit(r.d.z) ? 4 : 0);
     const DNodeC *nodes = sc.nodes + (size_t)oct * (size_t)sc.nnodes;
-    const double mx = FMA_SLAB ? -(r.o.x * inv.x) : 0.0, my = FMA_SLAB ? -(r.o.y * inv.y) : 0.0,
-                 mz = FMA_SLAB ? -(r.o.z * inv.z) : 0.0;
+    // (FMA_SLAB) -o/d can overflow while 1/d is finite (|d| below ~|o| / 1.8e308): the axis's plane t's would be
+    // +-inf and cull the node that holds the hit, so such an axis is left open for this ray (a NaN -o/d makes
+    // every t of the axis NaN, which drops out of fmax/fmin): conservative, like an infinite 1/d
+    auto open_inf = [](double m) { return __builtin_isinf(m) ? __builtin_nan("") : m; };
+    const double mx = FMA_SLAB ? open_inf(-(r.o.x * inv.x)) : 0.0, my = FMA_SLAB ? open_inf(-(r.o.y * inv.y)) : 0.0,
+                 mz = FMA_SLAB ? open_inf(-(r.o.z * inv.z)) : 0.0;
     auto tx = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.x, mx) : ((double)b - r.o.x) * inv.x; };
     auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
     auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };

@@ -15,20 +15,27 @@
 
 namespace {
 
-uint32_t crc_table[256];
-bool crc_ready = false;
-
-void crc_init() {
-    for (uint32_t n = 0; n < 256; n++) {
-        uint32_t c = n;
-        for (int k = 0; k < 8; k++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-        crc_table[n] = c;
+struct CrcTable {
+    uint32_t t[256];
+    CrcTable() {
+        for (uint32_t n = 0; n < 256; n++) {
+            uint32_t c = n;
+            for (int k = 0; k < 8; k++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+            t[n] = c;
+        }
     }
-    crc_ready = true;
+};
+
+// built once, on first use, by whichever thread gets there first (a function-local static's initialisation is
+// thread-safe): pt_write_png may be called from several host threads at once
+const uint32_t *crc_table() {
+    static const CrcTable table;
+    return table.t;
 }
 
 uint32_t crc32(const uint8_t *p, size_t n, uint32_t c = 0xFFFFFFFFu) {
-    for (size_t i = 0; i < n; i++) c = crc_table[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    const uint32_t *tab = crc_table();
+    for (size_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
     return c;
 }
 
@@ -77,7 +84,13 @@ int pt_write_png(const char *path, const uint8_t *rgba, uint32_t width, uint32_t
         pt_set_last_error("pt_write_png: null argument or empty image");
         return PT_ERR_INVALID;
     }
-    if (!crc_ready) crc_init();
+    // a PNG chunk's length is a 32-bit field (and < 2^31 by the spec): the one IDAT chunk must fit
+    const size_t row = (size_t)width * 4;
+    const size_t raw_bytes = (row + 1) * height;
+    if (raw_bytes + raw_bytes / 65535 * 5 + 64 >= ((size_t)1 << 31)) {
+        pt_set_last_error("pt_write_png: image too large for one IDAT chunk");
+        return PT_ERR_INVALID;
+    }
     std::vector<uint8_t> png = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
     std::vector<uint8_t> ihdr;
     be32(ihdr, width);
@@ -85,9 +98,8 @@ int pt_write_png(const char *path, const uint8_t *rgba, uint32_t width, uint32_t
     ihdr.insert(ihdr.end(), {8, 6, 0, 0, 0});  // 8 bit, RGBA, deflate, filter method 0, no interlace
     chunk(png, "IHDR", ihdr);
     // raw scanlines: filter type 0 (None) then the row's RGBA bytes
-    const size_t row = (size_t)width * 4;
     std::vector<uint8_t> raw;
-    raw.reserve((row + 1) * height);
+    raw.reserve(raw_bytes);
     for (uint32_t y = 0; y < height; y++) {
         raw.push_back(0);
         raw.insert(raw.end(), rgba + (size_t)y * row, rgba + (size_t)(y + 1) * row);

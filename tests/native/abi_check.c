@@ -3,12 +3,15 @@
  *
  *   abi_check layout                 sizeof / offsetof of every boundary struct as
  *                                    this compiler lays it out == pt_abi_layout
- *   abi_check legacy <scene.json>    a version-1 caller: the 16-byte
- *                                    {random_spheres, reserved = 0, seed} struct at the
- *                                    very end of a readable page, the next page
- *                                    PROT_NONE, so a read past it faults; the scene
- *                                    (with an ImageTexture) must load, and a
- *                                    struct_size below 16 must be refused
+ *   abi_check legacy <scene.json>    a 0.1.0 / 0.2.0 caller: the 32-byte struct with
+ *                                    `reserved` = 0 where struct_size now sits and an
+ *                                    image loader set, at the very end of a readable
+ *                                    page, the next page PROT_NONE, so a read past it
+ *                                    faults; the scene (with an ImageTexture) must load
+ *                                    through that loader, never the built-in reader; a
+ *                                    16-byte struct (struct_size 16) must load without
+ *                                    reading past it; a struct_size below 16 must be
+ *                                    refused
  *   abi_check render <scene.json> <w> <h> <spp> <depth> <seed> <out.f64>
  *                                    Scene::from_json -> ThreadPoolRenderer::new ->
  *                                    start_rendering -> render_step (blocking) through
@@ -98,12 +101,25 @@ static int do_layout(void) {
     return bad;
 }
 
-/* the version-1 options struct (0.2.0 and earlier): 16 bytes */
+/* the options struct of 0.1.0 / 0.2.0: 32 bytes, `reserved` always 0 */
 typedef struct {
     uint32_t random_spheres;
     uint32_t reserved;
     uint64_t seed;
-} opts_v1;
+    pt_image_loader load_image;
+    void *image_user;
+} opts_v02;
+
+/* an image loader that answers every file with a 2x2 RGBA8 image and counts its calls */
+static const uint8_t tiny_rgba[16] = {255, 0, 0, 255, 0, 255, 0, 255, 0, 0, 255, 255, 255, 255, 255, 255};
+static int counting_loader(void *user, const char *filename, uint32_t *w, uint32_t *h, const uint8_t **rgba8) {
+    (void)filename;
+    ++*(int *)user;
+    *w = 2;
+    *h = 2;
+    *rgba8 = tiny_rgba;
+    return PT_OK;
+}
 
 static int do_legacy(const char *path) {
     size_t len = 0;
@@ -118,22 +134,43 @@ static int do_legacy(const char *path) {
         fprintf(stderr, "mmap / mprotect failed\n");
         return 1;
     }
-    opts_v1 *o = (opts_v1 *)(mem + pg - sizeof(opts_v1));  /* the next byte is unreadable */
+    int calls = 0;
+    opts_v02 *o = (opts_v02 *)(mem + pg - sizeof(opts_v02));  /* the next byte is unreadable */
     o->random_spheres = 1;
     o->reserved = 0;
     o->seed = 7;
+    o->load_image = counting_loader;
+    o->image_user = &calls;
     pt_scene *s = NULL;
     int rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o, &s);
     if (rc != PT_OK) {
-        fprintf(stderr, "version-1 opts: status %d: %s\n", rc, pt_last_error());
+        fprintf(stderr, "0.2.0 opts: status %d: %s\n", rc, pt_last_error());
         return 1;
     }
-    printf("version-1 opts: %d shapes, %d materials\n", pt_scene_num_shapes(s), pt_scene_num_materials(s));
+    if (calls == 0) {
+        fprintf(stderr, "0.2.0 opts: the caller's image loader was not used\n");
+        return 1;
+    }
+    printf("0.2.0 opts: %d shapes, %d materials, loader called %d times\n", pt_scene_num_shapes(s),
+           pt_scene_num_materials(s), calls);
     pt_scene_destroy(s);
-    /* a struct_size that cannot hold even the version-1 fields */
-    o->reserved = 8;
+    /* the 16 bytes {random_spheres, struct_size = 16, seed} against the page end: no loader is read */
+    uint32_t *o16 = (uint32_t *)(mem + pg - 16);
+    o16[0] = 1;
+    o16[1] = 16;
+    *(uint64_t *)(o16 + 2) = 7;
     s = NULL;
-    rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o, &s);
+    rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o16, &s);
+    if (rc != PT_OK) {
+        fprintf(stderr, "16-byte opts: status %d: %s\n", rc, pt_last_error());
+        return 1;
+    }
+    printf("16-byte opts: %d shapes\n", pt_scene_num_shapes(s));
+    pt_scene_destroy(s);
+    /* a struct_size that cannot hold even {random_spheres, struct_size, seed} */
+    o16[1] = 8;
+    s = NULL;
+    rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o16, &s);
     if (rc != PT_ERR_INVALID || s) {
         fprintf(stderr, "struct_size 8 accepted (status %d)\n", rc);
         return 1;

@@ -115,15 +115,18 @@ def test_plain_c_caller_layout():
     assert out.stdout.count("match") == 5
 
 
-def test_version1_opts_are_not_read_past():
-    """A 16-byte version-1 pt_scene_opts placed against an unreadable page: the
-    scene (with an ImageTexture, whose loader field a version-1 struct does not
-    have) loads without touching the page; struct_size 8 is refused."""
+def test_legacy_opts_keep_their_loader_and_are_not_read_past():
+    """A 0.2.0 caller's 32-byte pt_scene_opts (`reserved` = 0 where struct_size
+    sits now, an image loader set) placed against an unreadable page: the scene
+    (with an ImageTexture) loads through that loader, not the built-in reader;
+    a 16-byte struct (struct_size 16) loads without touching the page;
+    struct_size 8 is refused (no silent fallback for old callers)."""
     import subprocess
     out = subprocess.run([abi_check_bin(), "legacy", "scenes/textured.json"], capture_output=True, text=True,
                          cwd=str(ROOT))
     assert out.returncode == 0, (out.returncode, out.stderr)
     assert "struct_size 8 refused" in out.stdout
+    assert "loader called" in out.stdout and "16-byte opts" in out.stdout
 
 
 def test_opts_struct_size_from_python(pt, cornell_text):

@@ -128,7 +128,10 @@ def test_stop_waits_only_for_running_launches(pt, cornell):
     r.stop_rendering()
     t_stop = time.perf_counter() - t0
     print("stop of a 3840x2160 1024 spp frame after 0.8 s: %.1f ms" % (t_stop * 1e3))
-    assert t_stop < 0.2, t_stop
+    # the evidence is the logged time (5-8 ms on an idle box, profiles/r3/stop_probe_c3size.txt); the bound
+    # only has to separate "queued launches skipped" from "queued launches drained": draining the running
+    # band and the queued one takes ~0.5-1 s, so a loaded shared box cannot fail a working stop
+    assert t_stop < 0.4, t_stop
     w2, h2 = 320, 180
     buf = np.zeros((w2 * h2, 3))
     r.start_rendering(cam, pt.ImageParams(w2, h2), 4, seed=1)
@@ -301,6 +304,29 @@ def test_tuning_options(pt, cornell):
         r.set_option("wf_slots", 1)  # not while a frame is in flight
     r.stop_rendering()
     assert np.array_equal(base, osc.render(64, 40, 3, 8, 4, threads=host_threads()))
+
+
+def test_failed_bvh_rebuild_keeps_the_old_tree(pt, cornell):
+    """A BVH rebuild (set_option bvh_leaf) whose upload fails on one device (an
+    injected allocation failure, the test hook fault_accel_alloc) leaves every
+    device on its old, complete tree: the option keeps its value and frames
+    stay bit-exact; a later rebuild succeeds."""
+    ps, osc = cornell
+    r = pt.HipRenderer(ps, depth=8, devices=[0, 0])  # two device shares (a repeated ordinal on the test box)
+    cam, ip = ps.camera(), pt.ImageParams(64, 40)
+    ref = osc.render(64, 40, 2, 8, 5, threads=host_threads())
+    leaf0 = r.get_option("bvh_leaf")
+    # 5 allocations per device: the first device's 1st and 3rd, the second device's 2nd
+    for fault_at in (1, 3, 7):
+        r.set_option("fault_accel_alloc", fault_at)
+        with pytest.raises(pt.PtError):
+            r.set_option("bvh_leaf", leaf0 + 1)
+        assert r.get_option("bvh_leaf") == leaf0
+        assert np.array_equal(r.render(cam, ip, 2, seed=5), ref), fault_at
+    r.set_option("fault_accel_alloc", 0)
+    r.set_option("bvh_leaf", leaf0 + 1)
+    assert r.get_option("bvh_leaf") == leaf0 + 1
+    assert np.array_equal(r.render(cam, ip, 2, seed=5), ref)
 
 
 def test_diagnostics_refused_while_a_frame_is_in_flight(pt, cornell):

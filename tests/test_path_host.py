@@ -256,3 +256,44 @@ def test_bvh_fma_slab_build_same_hits(H):
         assert (w0, t0.value) == (w1, t1.value), (o, d)
         hits += w0 >= 0
     assert hits > 1000
+
+
+def test_bvh_fma_slab_tiny_direction_component(H):
+    """FMA_SLAB with a direction component so small that 1/d is finite but o/d
+    overflows (|d| ~ 1e-308, |o| ~ 10): the plane t's of that axis must not
+    become +-inf and cull the node that holds the hit.  Both
+    builds must return the oracle's closest hit."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    H.h_closest_nomarch.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    scene = make_scenes.synthetic(3000)
+    pr = Pair(H, json.dumps(scene), seed=1)
+    rng = np.random.default_rng(23)
+    centres = [np.array(s["transform"]["translate"], float) for s in scene["shapes"][1:]]
+    hits = 0
+    for _ in range(600):
+        c = centres[rng.integers(len(centres))]
+        if max(abs(c[0]), abs(c[2])) < 3:
+            continue
+        ax = 0 if abs(c[2]) > abs(c[0]) else 2  # travel along an axis; the tiny component on the large one
+        tiny = 2 - ax
+        o = c.copy()
+        o[ax] -= rng.choice([-1.0, 1.0]) * 1.5
+        o[1] += rng.uniform(-0.1, 0.1)
+        o[tiny] += rng.uniform(-0.1, 0.1)
+        d = np.zeros(3)
+        d[ax] = 1.0 if c[ax] > o[ax] else -1.0
+        d[tiny] = rng.choice([1e-308, -1e-308, 3e-308, -5e-309])
+        ray6 = np.concatenate([o, d])
+        ray = (C.c_double * 6)(*ray6)
+        ref = pr.o.closest_hit(o, d)
+        for fma in (0, 1):
+            t = C.c_double()
+            w = H.h_closest_nomarch(pr.h, ray, fma, C.byref(t))
+            if ref is None:
+                assert w == -1, (fma, ray6)
+            else:
+                assert (w, t.value) == (ref.shape, ref.t), (fma, ray6, w, ref.shape)
+        hits += ref is not None
+    assert hits > 200

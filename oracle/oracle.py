@@ -19,7 +19,8 @@ from pathlib import Path
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "_build" / "liboracle.so"
+# PT_ORACLE_LIB: another build of the same source (the sanitizer build, scripts/san.sh)
+LIB_PATH = Path(os.environ["PT_ORACLE_LIB"]) if os.environ.get("PT_ORACLE_LIB") else HERE / "_build" / "liboracle.so"
 
 SPHERE, RECT, CUBE, MARCH, TORUS = 0, 1, 2, 3, 4
 FUNC_HEART, FUNC_SINE, FUNC_STAR, FUNC_DUPIN, FUNC_HUNTS, FUNC_CUSHION = 0, 1, 2, 3, 4, 5

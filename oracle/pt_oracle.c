@@ -1466,8 +1466,11 @@ int or_render(const or_scene *sc, const or_caster *k, uint32_t spp, uint32_t dep
     j.want_stats = st != NULL;
     pthread_mutex_init(&j.lock, NULL);
     pthread_t *tid = malloc(sizeof(pthread_t) * threads);
-    for (int i = 0; i < threads; i++) pthread_create(&tid[i], NULL, worker, &j);
-    for (int i = 0; i < threads; i++) pthread_join(tid[i], NULL);
+    int started = 0;
+    if (tid)
+        while (started < threads && pthread_create(&tid[started], NULL, worker, &j) == 0) started++;
+    if (started == 0) worker(&j); /* no thread could start: the caller's thread pulls every chunk */
+    for (int i = 0; i < started; i++) pthread_join(tid[i], NULL);
     free(tid);
     pthread_mutex_destroy(&j.lock);
     if (st) *st = j.stats;

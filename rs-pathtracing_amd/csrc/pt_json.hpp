@@ -1,8 +1,13 @@
 // pt_json.hpp — minimal JSON reader for the scene schema (the role serde_json
 // plays for Scene::from_json, src/world/mod.rs:46-49).  Numbers are parsed with
-// strtod (correctly rounded, like serde_json on the values scenes use).
+// std::from_chars (correctly rounded, like serde_json on the values scenes use,
+// and independent of the host application's locale, which strtod is not).
+// Nesting is limited to 128 levels, serde_json's default recursion limit, so a
+// hostile file cannot exhaust the caller's stack.
 #pragma once
 
+#include <charconv>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -49,7 +54,9 @@ class Parser {
     }
 
   private:
+    static constexpr int kMaxDepth = 128;  // serde_json's recursion limit
     const char *p_, *end_, *begin_;
+    int depth_ = 0;
 
     [[noreturn]] void fail(const std::string &what) {
         size_t line = 1, col = 1;
@@ -74,13 +81,26 @@ class Parser {
         }
         return false;
     }
+    struct Nest {  // one level of array / object nesting
+        Parser &p;
+        explicit Nest(Parser &q) : p(q) {
+            if (++p.depth_ > kMaxDepth) p.fail("recursion limit exceeded");
+        }
+        ~Nest() { --p.depth_; }
+    };
     Value value() {
         ws();
         if (p_ >= end_) fail("EOF while parsing a value");
         Value v;
         char c = *p_;
-        if (c == '{') return object();
-        if (c == '[') return array();
+        if (c == '{') {
+            Nest n(*this);
+            return object();
+        }
+        if (c == '[') {
+            Nest n(*this);
+            return array();
+        }
         if (c == '"') {
             v.kind = Value::String;
             v.str = string();
@@ -122,12 +142,47 @@ class Parser {
             if (p_ >= end_ || !(*p_ >= '0' && *p_ <= '9')) fail("invalid number");
             while (p_ < end_ && *p_ >= '0' && *p_ <= '9') ++p_;
         }
-        std::string tok(s, p_);
         Value v;
         v.kind = Value::Number;
-        v.num = std::strtod(tok.c_str(), nullptr);
+        const auto r = std::from_chars(s, p_, v.num);  // JSON's grammar is a subset of from_chars' general format
+        if (r.ec == std::errc::result_out_of_range) {
+            // serde_json: an overflow is "number out of range", an underflow rounds to a (signed) zero
+            if (decimal_exponent(s, p_) >= 0) fail("number out of range");
+            v.num = *s == '-' ? -0.0 : 0.0;
+        } else if (r.ec != std::errc() || r.ptr != p_) {
+            fail("invalid number");
+        }
         v.is_integer = integer;
         return v;
+    }
+    // floor(log10 |x|) of a valid JSON number literal with a non-zero digit (else -1): the position of its
+    // first non-zero digit relative to the decimal point, plus the explicit exponent
+    static long decimal_exponent(const char *s, const char *e) {
+        const char *q = *s == '-' ? s + 1 : s;
+        long int_digits = 0, first_int = 0, frac_place = 0, mag = 0;
+        bool frac = false, seen = false;
+        for (; q < e && *q != 'e' && *q != 'E'; ++q) {
+            if (*q == '.') {
+                frac = true;
+            } else if (!frac) {
+                int_digits++;
+                if (!seen && *q != '0') seen = true, first_int = int_digits;
+            } else {
+                frac_place++;
+                if (!seen && *q != '0') seen = true, mag = -frac_place;
+            }
+        }
+        if (!seen) return -1;
+        if (first_int) mag = int_digits - first_int;
+        long exp10 = 0;
+        if (q < e) {  // exponent part
+            ++q;
+            bool neg = false;
+            if (*q == '+' || *q == '-') neg = *q++ == '-';
+            for (; q < e; ++q) exp10 = exp10 < 100000000 ? exp10 * 10 + (*q - '0') : exp10;
+            if (neg) exp10 = -exp10;
+        }
+        return mag + exp10;
     }
     static void put_utf8(std::string &o, unsigned cp) {
         if (cp < 0x80) {
@@ -184,9 +239,11 @@ class Parser {
             case 't': o += '\t'; break;
             case 'u': {
                 unsigned cp = hex4();
+                if (cp >= 0xDC00 && cp < 0xE000) fail("lone trailing surrogate in hex escape");
                 if (cp >= 0xD800 && cp < 0xDC00) {
-                    if (!(lit("\\u"))) fail("lone surrogate");
+                    if (!(lit("\\u"))) fail("lone leading surrogate in hex escape");
                     unsigned lo = hex4();
+                    if (lo < 0xDC00 || lo >= 0xE000) fail("invalid low surrogate in hex escape");
                     cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
                 }
                 put_utf8(o, cp);

@@ -37,6 +37,14 @@ def oracle_mod():
     return oracle
 
 
+# the host builds of tests/native: _build, or the sanitizer build _build_san (scripts/san.sh sets PT_NATIVE_BUILD)
+NATIVE_BUILD = ROOT / "tests" / "native" / __import__("os").environ.get("PT_NATIVE_BUILD", "_build")
+
+
+def native_lib(name):
+    return str(NATIVE_BUILD / name)
+
+
 def scene_text(name):
     return (ROOT / "scenes" / name).read_text()
 

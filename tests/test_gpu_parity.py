@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import native_lib
 
 pytestmark = pytest.mark.gpu
 
@@ -309,7 +310,7 @@ def test_count_work_matches_host_build(pt, cornell, cornell_text):
     from pathlib import Path
     native = Path(__file__).resolve().parent / "native"
     subprocess.run(["make", "-s", "-C", str(native)], check=True)
-    L = C.CDLL(str(native / "_build" / "libpath.so"))
+    L = C.CDLL(native_lib("libpath.so"))
     L.h_scene_new.restype = C.c_void_p
     L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]
     L.h_count_work.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,

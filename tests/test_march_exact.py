@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import native_lib
 
 NATIVE = Path(__file__).resolve().parent / "native"
 
@@ -19,7 +20,7 @@ NATIVE = Path(__file__).resolve().parent / "native"
 @pytest.fixture(scope="module")
 def march_lib():
     subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
-    L = C.CDLL(str(NATIVE / "_build" / "libmarch.so"))
+    L = C.CDLL(native_lib("libmarch.so"))
     d = C.POINTER(C.c_double)
     L.march_heart.argtypes = [C.c_double, C.c_int, d, d, d, C.c_double, C.c_double, d,
                               C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]

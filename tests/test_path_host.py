@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import native_lib
 
 NATIVE = Path(__file__).resolve().parent / "native"
 
@@ -18,7 +19,7 @@ NATIVE = Path(__file__).resolve().parent / "native"
 @pytest.fixture(scope="module")
 def H():
     subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
-    L = C.CDLL(str(NATIVE / "_build" / "libpath.so"))
+    L = C.CDLL(native_lib("libpath.so"))
     d = C.POINTER(C.c_double)
     L.h_scene_new.restype = C.c_void_p
     L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]

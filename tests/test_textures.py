@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import native_lib
 
 ROOT = Path(__file__).resolve().parent.parent
 NATIVE = ROOT / "tests" / "native"
@@ -165,7 +166,7 @@ def test_loader_rejects_bad_textures(pt):
 @pytest.fixture(scope="module")
 def H():
     subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
-    L = C.CDLL(str(NATIVE / "_build" / "libpath.so"))
+    L = C.CDLL(native_lib("libpath.so"))
     d = C.POINTER(C.c_double)
     L.h_scene_new.restype = C.c_void_p
     L.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]

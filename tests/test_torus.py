@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from conftest import native_lib
 
 ROOT = Path(__file__).resolve().parent.parent
 NATIVE = ROOT / "tests" / "native"
@@ -79,7 +80,7 @@ def test_loader_takes_torus(pt):
 
 def test_host_build_matches_oracle_on_torus_frames():
     subprocess.run(["make", "-s", "-C", str(NATIVE)], check=True)
-    H = C.CDLL(str(NATIVE / "_build" / "libpath.so"))
+    H = C.CDLL(native_lib("libpath.so"))
     d = C.POINTER(C.c_double)
     H.h_scene_new.restype = C.c_void_p
     H.h_scene_new.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_uint64]

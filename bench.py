@@ -217,20 +217,50 @@ def parity_pixels(args):
     return np.unique(np.concatenate([grid, row, col])).astype(np.uint32)
 
 
-def profile_file(name, workload, source):
-    """A committed PMC result (profiles/rN/<name>) of this workload, newest round first, and whether it was
-    collected on this build (its source_id == the loaded library's): (path, record, why_not)."""
-    for rnd in ("r3", "r2", "r1"):
-        f = ROOT / "profiles" / rnd / name
-        if f.exists():
-            tr = json.loads(f.read_text())
-            if tr.get("workload") != workload:
+ROUNDS = ("r4", "r3", "r2", "r1")  # profiles/<round>/, newest first
+
+
+def parse_workload(w):
+    """"cornell_box.json 1920x1080 256spp depth 8" -> (scene, width, height, spp, depth), or None."""
+    import re
+    m = re.fullmatch(r"(\S+) (\d+)x(\d+) (\d+)spp depth (\d+)", w or "")
+    return (m.group(1), int(m.group(2)), int(m.group(3)), int(m.group(4)), int(m.group(5))) if m else None
+
+
+def pmc_lookup(what, scene, depth, width, height, spp, source, root=ROOT):
+    """A committed PMC result (profiles/rN/pmc_<what>_*.json, what = flops | traffic) for this scene and depth,
+    collected on this build (its source_id == the loaded library's).  FLOPs and HBM bytes per sample depend on
+    the scene, the depth and the machine code, not on the frame size or spp: every sample runs the same path
+    (trace_pixel_samples, src/renderer/mod.rs:151-155), and the chunked engine's bytes per path-bounce do not
+    depend on how many chunks a frame has (measured: C2 and C3 agree within 0.1 %).  So a pass of any resolution
+    and spp of the same (scene, depth, build) serves every config: the exact workload first, then the newest
+    round.  Returns (path, record, samples_per_frame_of_the_pass, why_not)."""
+    found, builds = [], set()
+    for rank, rnd in enumerate(ROUNDS):
+        d = root / "profiles" / rnd
+        if not d.is_dir():
+            continue
+        for f in sorted(d.glob("pmc_%s_*.json" % what)):
+            try:
+                rec = json.loads(f.read_text())
+            except (OSError, ValueError):
                 continue
-            if tr.get("source_id") != source:
-                return f, None, "%s was collected on build %s, this is %s" % (f.relative_to(ROOT),
-                                                                             tr.get("source_id"), source)
-            return f, tr, None
-    return None, None, "no committed %s for this workload" % name
+            wl = parse_workload(rec.get("workload"))
+            if not wl or (wl[0], wl[4]) != (scene, depth):
+                continue
+            builds.add(rec.get("source_id"))
+            if rec.get("source_id") != source:
+                continue
+            exact = (wl[1], wl[2], wl[3]) == (width, height, spp)
+            found.append((not exact, rank, f, rec, float(rec.get("samples_per_frame") or wl[1] * wl[2] * wl[3])))
+    if not found:
+        why = ("no committed pmc_%s file for %s depth %d" % (what, scene, depth) if not builds else
+               "pmc_%s files for %s depth %d were collected on build(s) %s, this is %s"
+               % (what, scene, depth, ", ".join(sorted(str(b) for b in builds)), source))
+        return None, None, None, why
+    found.sort(key=lambda c: (c[0], c[1]))
+    _, _, f, rec, spf = found[0]
+    return f, rec, spf, None
 
 
 def main():
@@ -384,9 +414,8 @@ def main():
         workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
         # algorithmic FLOPs per sample: from the f64 instruction counters of a committed PMC pass of this
         # workload (scripts/pmc_flops.py) when there is one, else the event counts times FLOP_WEIGHTS
-        cfg = args.config or ("c2" if metric_name(args) == METRIC else None)
         src_id = pt.source_id()
-        ff, fl, f_why = profile_file("pmc_flops_%s.json" % cfg, workload, src_id) if cfg else (None, None, "no config")
+        ff, fl, _, f_why = pmc_lookup("flops", args.scene, args.depth, W, H, spp, src_id)
         f_kind = dict(f_weights)
         if fl:
             for k, v in fl["kinds"].items():
@@ -431,9 +460,10 @@ def main():
                                       if kt_iso is not None else "timed steps (launches of two chunk streams overlap)"),
                          "kernels": per_kernel,
                          "flops_per_sample_total": round(F, 1),
-                         "flops_source": ("f64 instruction counters x mean active lanes, %s (scripts/pmc_flops.py); "
+                         "flops_source": ("f64 instruction counters x mean active lanes, %s (%s; scripts/pmc_flops.py); "
                                           "event weights give %.1f FLOP/sample (%.2fx)"
-                                          % (ff.relative_to(ROOT), f_weights["bounce"] + f_weights["march"],
+                                          % (ff.relative_to(ROOT), fl["workload"],
+                                             f_weights["bounce"] + f_weights["march"],
                                              (f_weights["bounce"] + f_weights["march"]) / F) if fl else
                                           "kernel event counters (pt_count_work) x FLOP_WEIGHTS (%s)" % f_why),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
@@ -472,24 +502,24 @@ def main():
             rec["tuning"] = tuning
         # roofline.traffic: HBM bytes per launch of the same kernel from the committed PMC passes of this
         # workload (scripts/pmc_traffic.py; bench.py cannot read PMC counters itself)
-        tf, tr, t_why = profile_file("pmc_traffic_%s.json" % cfg, workload, src_id) if cfg else (None, None, "no config")
+        tf, tr, t_spf, t_why = pmc_lookup("traffic", args.scene, args.depth, W, H, spp, src_id)
         if not tr:
             rec["roofline"]["traffic_source"] = t_why
-        if tr and world == 1 and not multi:
-            kind = tr.get("kinds", {}).get(dom)
-            if kind:
-                # the PMC pass's bytes per frame (launches x bytes per launch) spread over this frame's launches
-                # of the kernel: bytes per sample do not depend on the chunking, bytes per launch do
-                frame_bytes = kind["traffic"] * kind.get("launches", dom_n // nfr)
-                per_launch = frame_bytes / max(1, dom_n // nfr)
-                rec["roofline"]["traffic"] = round(per_launch)
-                rec["roofline"]["traffic_source"] = "%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % tf.relative_to(ROOT)
-                rec["roofline"]["traffic_gbs"] = round(per_launch / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
-                rec["roofline"]["traffic_per_sample"] = round(frame_bytes / (W * H * spp), 1)
-                if kind.get("launches") not in (None, dom_n // nfr):
-                    rec["roofline"]["traffic_note"] = ("PMC pass: %s launches per frame (two chunk streams); %d here: "
-                                                       "its bytes per frame spread over them" % (kind["launches"],
-                                                                                                 dom_n // nfr))
+        kind = tr.get("kinds", {}).get(dom) if tr else None
+        if kind:
+            # bytes per sample of the pass (its launches x bytes per launch over its samples), times the samples
+            # this rank's (or first device's) launches of the kernel processed, per launch: bytes per sample do
+            # not depend on the chunking or the frame size, bytes per launch do
+            per_sample = kind["traffic"] * kind["launches"] / (t_spf * tr.get("frames", 1))
+            per_launch = per_sample * samples_share * nfr / max(1, dom_n)
+            rec["roofline"]["traffic"] = round(per_launch)
+            rec["roofline"]["traffic_source"] = ("%s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, %s)"
+                                                 % (tf.relative_to(ROOT), tr["workload"]))
+            rec["roofline"]["traffic_gbs"] = round(per_launch / (dom_ms / max(1, dom_n) / 1e3) / 1e9, 1)
+            rec["roofline"]["traffic_per_sample"] = round(per_sample, 1)
+            if world > 1 or multi:
+                rec["roofline"]["traffic_note"] = "per launch of this rank's share (%d of %d tiles)" % (
+                    per_rank_tiles[0], pt.shard_tiles(W, H, 0, 1))
         if not args.no_parity:
             import oracle
             px = parity_pixels(args)

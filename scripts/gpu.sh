@@ -44,7 +44,7 @@ pmc)
         > $OUT/fetch.log 2>&1
     prof --kernel-trace --output-format csv -d $OUT/write -o p "${FILT[@]}" --pmc WRITE_SIZE -- python3 $R/bench.py "$@" \
         > $OUT/write.log 2>&1
-    python3 scripts/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json "${WORKLOAD:-cornell_box.json 1920x1080 256spp depth 8}" \
+    python3 scripts/pmc_traffic.py $OUT/fetch $OUT/write $OUT/pmc_traffic.json "${WORKLOAD:-cornell_box.json 1920x1080 256spp depth 8}" ${PMC_FRAMES:-1} \
         > $OUT/traffic.log ;;
 sq)
     prof --kernel-trace --output-format csv -d $OUT/sq -o p "${FILT[@]}" --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \

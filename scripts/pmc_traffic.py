@@ -1,6 +1,10 @@
 """HBM bytes per launch of each render kernel kind from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
-Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON WORKLOAD
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON WORKLOAD [FRAMES]
+
+FRAMES: frames of WORKLOAD the passes ran (default 1); bench.py turns the bytes into bytes per sample
+(launches x bytes per launch / (frames x samples per frame)) and uses them for any frame size and spp of the
+same scene, depth and build.
 
 Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): both counters are in KiB; on gfx950 FETCH_SIZE reports
 half the bytes of a wide coalesced read, so it is doubled; WRITE_SIZE is taken as is. bench.py reads OUT_JSON
@@ -47,9 +51,10 @@ def collect(d, counter):
 
 def main():
     fetch_dir, write_dir, out, workload = sys.argv[1:5]
+    frames = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     fetch, nf = collect(fetch_dir, "FETCH_SIZE")
     write, nw = collect(write_dir, "WRITE_SIZE")
-    rec = {"workload": workload, "source_id": source_id(), "unit": "bytes per launch",
+    rec = {"workload": workload, "source_id": source_id(), "unit": "bytes per launch", "frames": frames,
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "kinds": {}}
     for k in sorted(set(fetch) & set(write)):

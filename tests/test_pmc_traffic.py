@@ -75,3 +75,63 @@ def test_committed_c2_flops_match_bench_workload():
     for kind in ("bounce", "march"):
         k = rec["kinds"][kind]
         assert 1 <= k["mean_active_lanes"] <= 64 and k["algorithmic_flops_per_sample"] > 0
+
+
+def _profile(root, rnd, name, workload, source, **extra):
+    d = root / "profiles" / rnd
+    d.mkdir(parents=True, exist_ok=True)
+    rec = {"workload": workload, "source_id": source, "kinds": {"bounce": {"launches": 10, "traffic": 100.0,
+                                                                           "algorithmic_flops_per_sample": 1.0}}}
+    rec.update(extra)
+    (d / name).write_text(json.dumps(rec))
+
+
+def test_pmc_lookup_keys_on_scene_depth_and_build(tmp_path):
+    """bench.py takes a committed PMC pass of the same (scene, depth, build) for any frame size and spp (FLOPs and
+    bytes per sample are per-sample quantities): the exact workload first, then the newest round; other builds,
+    scenes or depths never."""
+    import bench
+    _profile(tmp_path, "r3", "pmc_flops_c2.json", "cornell_box.json 1920x1080 256spp depth 8", "b1")
+    _profile(tmp_path, "r3", "pmc_flops_c3.json", "cornell_box.json 3840x2160 1024spp depth 8", "b1")
+    _profile(tmp_path, "r4", "pmc_flops_c2.json", "cornell_box.json 1920x1080 256spp depth 8", "b2")
+    _profile(tmp_path, "r4", "pmc_flops_d50.json", "cornell_box.json 1920x1080 256spp depth 50", "b1")
+    _profile(tmp_path, "r3", "pmc_flops_c5.json", "synthetic_100000 1920x1080 256spp depth 8", "b1")
+    look = lambda *a: bench.pmc_lookup("flops", *a, root=tmp_path)  # noqa: E731
+    f, rec, spf, why = look("cornell_box.json", 8, 3840, 2160, 1024, "b1")
+    assert f.name == "pmc_flops_c3.json" and spf == 3840 * 2160 * 1024 and why is None  # exact workload
+    f, rec, spf, why = look("cornell_box.json", 8, 3840, 2160, 4096, "b1")  # C4: no pass of its own
+    assert rec["source_id"] == "b1" and rec["workload"].endswith("depth 8")
+    f, rec, spf, why = look("cornell_box.json", 8, 3840, 2160, 4096, "b2")
+    assert f.parent.name == "r4" and f.name == "pmc_flops_c2.json"
+    f, rec, spf, why = look("cornell_box.json", 8, 1920, 1080, 256, "b9")
+    assert rec is None and "b9" in why and "b1" in why
+    f, rec, spf, why = look("cornell_box.json", 50, 1920, 1080, 256, "b1")
+    assert f.name == "pmc_flops_d50.json"
+    f, rec, spf, why = look("spheres.json", 8, 256, 256, 16, "b1")
+    assert rec is None and "no committed" in why
+
+
+def test_traffic_per_sample_is_frame_size_independent(tmp_path):
+    """The pass's bytes per sample (launches x bytes per launch / its samples) are what a C4 or a rank's share is
+    priced with: the frames key of a multi-frame pass divides them."""
+    import bench
+    wl = "cornell_box.json 1920x1080 256spp depth 8"
+    _profile(tmp_path, "r4", "pmc_traffic_c2.json", wl, "b1", frames=2)
+    f, rec, spf, why = bench.pmc_lookup("traffic", "cornell_box.json", 8, 3840, 2160, 4096, "b1", root=tmp_path)
+    k = rec["kinds"]["bounce"]
+    per_sample = k["traffic"] * k["launches"] / (spf * rec.get("frames", 1))
+    assert per_sample == 100.0 * 10 / (1920 * 1080 * 256 * 2)
+
+
+def test_committed_passes_serve_every_cornell_config():
+    """Every committed C2/C3 pass is a cornell depth-8 workload bench.py can key on; C4 (no pass of its own) finds
+    one of them for whatever build they were collected on."""
+    import bench
+    for rnd in ("r3", "r4"):
+        for f in sorted((ROOT / "profiles" / rnd).glob("pmc_*_c[23].json")):
+            rec = json.loads(f.read_text())
+            wl = bench.parse_workload(rec["workload"])
+            assert wl and wl[0] == "cornell_box.json" and wl[4] == 8, f
+            f2, rec2, _, why = bench.pmc_lookup(f.name.split("_")[1], "cornell_box.json", 8, 3840, 2160, 4096,
+                                                rec["source_id"])
+            assert rec2 is not None and rec2["source_id"] == rec["source_id"], why

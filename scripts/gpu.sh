@@ -19,8 +19,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$tag
 mkdir -p $OUT
 cd $R
-# PMC_FILTER (optional): a kernel-name regex; counter passes collect only those kernels' dispatches
-# (the c3 frame's ~4,000 dispatches crashed rocprofv3's counter collection in round 3 without it)
+# PMC_FILTER (optional): a kernel-name regex; counter passes collect only those kernels' dispatches.  Not needed
+# for C3: run its passes at --slots 4 (profiles/r4/c3_profiler_abort.txt: at one stream, ~8,300 dispatches on one
+# HSA queue per frame meet a profiler defect at the queue's ring wrap)
 FILT=(); if [ -n "$PMC_FILTER" ]; then FILT=(--kernel-include-regex "$PMC_FILTER"); fi
 prof() {  # rocprofv3 with the program itself after -- (no launcher hops)
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL ${PROF_TIMEOUT:-400} rocprofv3 "$@")

@@ -4,16 +4,21 @@ For world N, each rank r renders its round-robin tiles (render_device with
 rank r of N) into its compact shard; the N-GPU frame time is the slowest
 rank's plus the frame-end gather and un-interleave.  Running every rank's
 share on the one GPU we have gives the compute part without the other GPUs;
-the gather is modelled by a device-to-device copy of the gathered bytes
-(world * per-rank shard, 24 B per pixel slot) plus the unshard kernel, timed
-on the same GPU (an xGMI gather moves the same bytes over ~7 links at
-~150 GB/s each, so this is a lower bound on its cost, not a measurement):
+the gather is bounded from the link rate the design assumes (an
+MI355X has 7 xGMI links of ~153 GB/s, one to each other GPU of the node):
 
-    python scripts/rank_sim.py [--worlds 1,8] [--spp 256] [--reps 2]
+* lower bound: every rank's shard reaches rank 0 over its own link at once,
+  shard bytes / link rate, plus the un-interleave kernel timed here;
+* upper bound: the N-1 shards reach rank 0 one after another over one link,
+  (N-1) x shard bytes / link rate, plus the un-interleave;
+* a local device-to-device copy of the gathered bytes (round 3's model) is
+  reported beside them; it is faster than any link, so it is not a bound.
 
-Prints one JSON line per world: max/mean rank ms, the gather model's ms, and
-two projected strong-scaling efficiencies: compute-only t1 / (N * max_rank_ms)
-and with the modelled gather.  The driver's SCALE run measures the real one.
+    python scripts/rank_sim.py [--worlds 1,8] [--spp 256] [--reps 2] [--link-gbs 153]
+
+Prints one JSON line per world: max/mean rank ms, the gather bounds, and the
+projected strong-scaling efficiency t1 / (N * (max_rank_ms + gather)) for the
+compute alone and with each bound.  The driver's SCALE run measures the real one.
 """
 import argparse
 import json
@@ -33,13 +38,15 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ranks", default="", help="subset of ranks to time (default: all)")
+    ap.add_argument("--link-gbs", type=float, default=153.0, help="xGMI link rate per direction (GB/s)")
+    ap.add_argument("--scene", default="cornell_box.json")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="a renderer tuning option (pt_renderer_set_option), repeatable")
     a = ap.parse_args()
     import torch
     import __graft_entry__ as ge
     pt = ge.load_package()
-    text = (ROOT / "scenes" / "cornell_box.json").read_text()
+    text = (ROOT / "scenes" / a.scene).read_text()
     scene = pt.Scene.from_json(text, seed=1)
     r = pt.HipRenderer(scene, device=0, depth=8)
     for o in a.option:
@@ -71,9 +78,11 @@ def main():
         mx = max(ms)
         if world == 1:
             t1 = mx
-        gather_ms = 0.0
-        if world > 1:  # the frame-end gather (modelled as a local D2D copy) and the un-interleave
+        copy_ms = unshard_ms = 0.0
+        shard_bytes = 0
+        if world > 1:  # the frame-end gather's local-copy model and the un-interleave, timed separately
             per = pt.shard_tiles(W, H, 0, world)
+            shard_bytes = per * 256 * 3 * 8
             g = torch.zeros(world * per * 256 * 3, dtype=torch.float64, device="cuda")
             src = torch.zeros_like(g)
             frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
@@ -81,15 +90,24 @@ def main():
                 torch.cuda.synchronize()
                 t = time.perf_counter()
                 g.copy_(src)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
                 pt.unshard_device(g.data_ptr(), W, H, world, frame.data_ptr(), sp)
                 torch.cuda.synchronize()
                 if rep:
-                    gather_ms = min(gather_ms or 1e30, (time.perf_counter() - t) * 1e3)
+                    copy_ms = min(copy_ms or 1e30, (t2 - t) * 1e3)
+                    unshard_ms = min(unshard_ms or 1e30, (time.perf_counter() - t2) * 1e3)
+        link = a.link_gbs * 1e9
+        lb_ms = (shard_bytes / link * 1e3 + unshard_ms) if world > 1 else 0.0
+        ub_ms = ((world - 1) * shard_bytes / link * 1e3 + unshard_ms) if world > 1 else 0.0
         rec = {"world": world, "max_rank_ms": round(mx, 2), "mean_rank_ms": round(sum(ms) / len(ms), 2),
-               "gather_model_ms": round(gather_ms, 3), "msamples_s": round(W * H * spp / (mx + gather_ms) / 1e3, 1)}
+               "shard_bytes": shard_bytes, "unshard_ms": round(unshard_ms, 3),
+               "gather_link_lb_ms": round(lb_ms, 3), "gather_link_ub_ms": round(ub_ms, 3),
+               "gather_local_copy_ms": round(copy_ms + unshard_ms, 3),
+               "msamples_s_range": [round(W * H * spp / (mx + ub_ms) / 1e3, 1), round(W * H * spp / (mx + lb_ms) / 1e3, 1)]}
         if t1:
-            rec["projected_eff_compute_only"] = round(t1 / (world * mx), 3)
-            rec["projected_eff_with_gather_model"] = round(t1 / (world * (mx + gather_ms)), 3)
+            rec["projected_eff_compute_only"] = round(t1 / (world * mx), 4)
+            rec["projected_eff_range"] = [round(t1 / (world * (mx + ub_ms)), 4), round(t1 / (world * (mx + lb_ms)), 4)]
         print(json.dumps(rec), flush=True)
 
 

@@ -11,6 +11,7 @@
 
 #include <cstdint>
 
+#include "pt_lprof.hpp"
 #include "pt_march.hpp"
 #include "pt_torus.hpp"
 #include "pt_types.hpp"
@@ -189,6 +190,7 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
         const double tt = -oz / dz;
         if (tt < min_t || tt > max_t) return false;
+        PT_LP(RECT_ROWS);
         const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
         const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
         const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
@@ -350,6 +352,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
         if (any && wave_all(who >= 0)) break;
         const int i = uniform_index(uniform_load(&sc.lin[k]));
         const DShape s = uniform_shape(&sc.shapes[i]);
+        PT_LP(ULIST_SHAPE);
         if (s.type == CUBE || s.type == SPHERE) {
             // the padded world box first (12 FLOP with the caller's 1/d):
             // a miss there is a miss of the exact test, which costs a full
@@ -357,6 +360,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
             if (STATS) ct->c[C_NODE_SLABS]++;
             const DBox b = uniform_box(&sc.boxes[i]);
             if (!slab(b.lo, b.hi, r, inv, min_t, best)) continue;
+            PT_LP(UBOX_PASS);
         }
         double t;
         if (shape_test<STATS, march::F_ANY, false, EXT>(s, r, min_t, best, &t, ct) && (t < best || i > who)) {
@@ -394,14 +398,17 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     int n = any && who >= 0 ? sc.nnodes : 0;
     while (n < sc.nnodes) {
         const DNodeC nd = nodes[n];
+        PT_LP(BVH_NODE);
         if (STATS) ct->c[C_NODE_SLABS]++;
         const double tn = fmax(fmax(tx(nd.nr[0]), ty(nd.nr[1])), fmax(tz(nd.nr[2]), min_t));
         const double tf = fmin(fmin(tx(nd.fr[0]), ty(nd.fr[1])), fmin(tz(nd.fr[2]), best));
         if (tn <= tf) {
+            PT_LP(BVH_ENTER);
             const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24 & 0x7fu);
             const bool direct = nd.first_count >> 31;  // one-shape leaf: `first` is the shape id
             for (int k = 0; k < count; k++) {
                 int i = direct ? first : sc.leaf[first + k];
+                PT_LP(BVH_LEAF);
                 double t;
                 if (shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct) && (t < best || i > who)) {
                     best = t;
@@ -625,6 +632,7 @@ struct PhaseTimes {
 template <bool STATS = false>
 PT_HD V3 random_in_unit_sphere(Rng &rng, double s11, Ctr *ct = nullptr) {
     for (;;) {
+        PT_LP(REJECT_TRY);
         if (STATS) ct->c[C_REJECT_TRIES]++;
         double x = rng.uniform(-1.0, s11);
         double y = rng.uniform(-1.0, s11);
@@ -715,6 +723,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     }
     const DShape &s = sc.shapes[who];
     if (STATS) ct->c[C_HITS]++;
+    PT_LP(SHADE_HIT);
     Hit h = finish<FK>(s, ray, t);
     const DMaterial &m = sc.mats[s.material];
     if (tfin) *tfin = PT_STAMP();
@@ -726,6 +735,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     };
     V3 dir;
     if (m.type == LAMBERTIAN) {  // material.rs:41-54
+        PT_LP(LAMBERT);
         if (STATS) ct->c[C_LAMBERT]++;
         V3 u = normalize(random_in_unit_sphere<STATS>(rng, s11, ct));
         dir = add(h.n, u);
@@ -733,12 +743,14 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         if (EXT && m.tex >= 0) stk.push_val(textured());
         else stk.push((uint32_t)s.material);
     } else if (m.type == METAL) {  // :63-76
+        PT_LP(METAL);
         if (STATS) ct->c[C_METAL]++;
         V3 rf = reflect(ray.d, h.n);
         dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
         if (EXT && m.tex >= 0) stk.push_val(textured());
         else stk.push((uint32_t)s.material);
     } else if (m.type == DIELECTRIC) {  // :92-115
+        PT_LP(DIELECTRIC);
         if (STATS) ct->c[C_DIELECTRIC]++;
         double ratio = h.front ? 1.0 / m.ior : m.ior;
         double c = dot(neg(ray.d), h.n);
@@ -753,6 +765,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         }
         dir = refl ? reflect(ray.d, h.n) : refract(ray.d, h.n, ratio);
     } else {  // DiffuseLight / EmptyMaterial: no scatter, emitted()
+        PT_LP(EMIT);
         if (EXT && m.type == DIFFUSE_LIGHT && m.tex >= 0) *leaf = textured();
         else *leaf = m.type == DIFFUSE_LIGHT ? v3(m.emit[0], m.emit[1], m.emit[2]) : v3(0.0, 0.0, 0.0);
         return true;

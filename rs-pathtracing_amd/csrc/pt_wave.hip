@@ -294,6 +294,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
     const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
+    PT_LP_BEGIN();
 #ifdef PT_BOUNCE_LANES
     // Tuning builds only (with the diag build): wave cycles between
     // consecutive stamps, charged to the section the stamp ends and weighted
@@ -373,6 +374,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         // needing no march measured +0.8 % / -2.5 %, round 2.)
         bool need_march = false, long_job = false;
         if (live) {
+            PT_LP(LIVE);
             if (!FIRST) {
                 V3 leaf;
                 const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
@@ -380,6 +382,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 if (ended) {
                     // the leaf radiance and the stack depth; wf_reduce unwinds
                     // the attenuation stack (end_path)
+                    PT_LP(ENDED);
                     end_path(v, id, stk, leaf);
                     live = false;
                     PT_BSTAMP(3)
@@ -387,6 +390,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             }
         }
         if (live) {
+            PT_LP(TRACE);
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             best = __builtin_inf();
             who = -1;
@@ -402,11 +406,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const int s = dev::uniform_index(dev::uniform_load(&sc.march[k]));
                 const DBox bx = dev::uniform_box(&sc.boxes[s]);
                 if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
+                PT_LP(PRE_SLAB);
                 const DShape S = dev::uniform_shape(&sc.shapes[s]);
                 const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
                 double st, en;
                 need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
                 if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
+                    PT_LP(PRE_JOB);
                     // the 64 B record in four 16-byte non-temporal stores (as eight 8-byte ones: the
                     // same time; structure of arrays: slower, round 3 jo2)
                     typedef double d2v __attribute__((ext_vector_type(2)));
@@ -433,6 +439,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             }
             PT_BSTAMP(5)
             if (any && !need_march) {
+                PT_LP(ANY_END);
                 // its shade would end it at once (mod.rs:24-27, 42-44): black
                 // after a hit, the background after a miss; only paths whose
                 // answer needs a march go on to the last iteration
@@ -441,12 +448,14 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             }
         }
         // every input position's state is written (ended paths too: whole lines; storeab)
+        if (i < count) PT_LP(STORE);
         if (i < count)
             store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
         if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
+    PT_LP_END();
 #ifdef PT_BOUNCE_LANES
     if (DIAG && (threadIdx.x & 63) == 0)
         for (int k = 0; k < 7; k++) {
@@ -1514,6 +1523,20 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     ws->used = true;
     return hipSuccess;
 }
+
+#ifdef PT_LANE_PROF
+// Lane profile of the bounce kernel (pt_lprof.hpp): out[k] wave passes and out[N + k] active lanes summed at
+// profiling point k, N = the return value; clear: zero the counters afterwards.
+extern "C" int pt_lane_prof(unsigned long long *out, int clear) {
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(lprof::g_counts), sizeof(lprof::g_counts)) != hipSuccess)
+        return -1;
+    if (clear) {
+        static const unsigned long long z[2 * lprof::N_POINTS] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(lprof::g_counts), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return lprof::N_POINTS;
+}
+#endif
 
 #ifdef PT_MARCH_REGIONS
 // Region wave-cycles of the march kernel since the last clear (tuning builds).

@@ -236,6 +236,9 @@ DShape to_device(const HostShape &s) {
     d.inverse_normal = s.inverse_normal;
     d.depth = s.depth;
     d.func = s.func;
+    const double(&m)[4][4] = s.inverse;
+    d.axis = s.type == SPHERE && m[0][1] == 0.0 && m[0][2] == 0.0 && m[1][0] == 0.0 && m[1][2] == 0.0 &&
+             m[2][0] == 0.0 && m[2][1] == 0.0 && m[0][3] != 0.0 && m[1][3] != 0.0 && m[2][3] != 0.0;
     return d;
 }
 DMaterial to_device(const HostMaterial &m) {

@@ -95,66 +95,6 @@ struct Builder {
         out.nodes[me].skip = (int32_t)(out.nodes.size() - base);
     }
 
-    // 4-ary collapse of the binary tree below t (an inner node): its two
-    // children, then repeatedly the inner child with the largest box surface
-    // replaced by its own two children, up to four; returns the DNode4 index.
-    static double area(const DNode &n) {
-        const double x = n.hi[0] - n.lo[0], y = n.hi[1] - n.lo[1], z = n.hi[2] - n.lo[2];
-        return x * y + y * z + z * x;
-    }
-    static int32_t leaf_ref(const DNode &n, const std::vector<int32_t> &leaf) {
-        if (n.count == 1 && leaf[n.first] >= 0 && leaf[n.first] < (1 << 24)) return ~leaf[n.first];
-        if (n.first < 0 || n.first >= (1 << 24) || n.count < 1 || n.count > 127)
-            throw std::runtime_error("BVH leaf out of range for the wide node form");
-        return ~(int32_t)((uint32_t)n.count << 24 | (uint32_t)n.first);
-    }
-    int emit4(int t, int depth) {
-        std::vector<int> ch;
-        if (tree[t].left < 0) {
-            ch.push_back(t);  // the root is a leaf: one child
-        } else {
-            ch = {tree[t].left, tree[t].right};
-            while (ch.size() < 4) {
-                int pick = -1;
-                double best = -1.0;
-                for (size_t i = 0; i < ch.size(); i++)
-                    if (tree[ch[i]].left >= 0 && area(tree[ch[i]].n) > best) {
-                        best = area(tree[ch[i]].n);
-                        pick = (int)i;
-                    }
-                if (pick < 0) break;
-                const int c = ch[pick];
-                ch.erase(ch.begin() + pick);
-                ch.insert(ch.begin() + pick, {tree[c].left, tree[c].right});  // keeps the binary order
-            }
-        }
-        out.depth4 = std::max(out.depth4, depth);
-        const int me = (int)out.nodes4.size();
-        out.nodes4.push_back(DNode4{});
-        DNode4 n{};
-        n.n = (int32_t)ch.size();
-        for (int k = 0; k < 4; k++) {
-            for (int a = 0; a < 3; a++) {  // unused slots: an empty box (and k >= n)
-                n.lo[a][k] = 1.0e30f;
-                n.hi[a][k] = -1.0e30f;
-            }
-            n.child[k] = -1;
-        }
-        for (size_t k = 0; k < ch.size(); k++) {
-            const DNode &c = tree[ch[k]].n;
-            for (int a = 0; a < 3; a++) {
-                float lo = (float)c.lo[a], hi = (float)c.hi[a];
-                if ((double)lo > c.lo[a]) lo = std::nextafter(lo, -INFINITY);
-                if ((double)hi < c.hi[a]) hi = std::nextafter(hi, INFINITY);
-                n.lo[a][k] = lo;
-                n.hi[a][k] = hi;
-            }
-            n.child[k] = tree[ch[k]].left < 0 ? leaf_ref(c, out.leaf) : emit4(ch[k], depth + 1);
-        }
-        out.nodes4[me] = n;
-        return me;
-    }
-
     int emit(std::vector<int32_t> &ids, size_t a, size_t b) {
         const int me = (int)tree.size();
         tree.push_back(TNode{DNode{}, 0, -1, -1});
@@ -200,7 +140,7 @@ struct Builder {
 
 }  // namespace
 
-Accel build_accel(const Scene &sc, int json_shapes, int leaf_max, int wide_min_nodes) {
+Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
     Accel a;
     a.boxes.reserve(sc.shapes.size());
     for (auto &s : sc.shapes) a.boxes.push_back(shape_box(s));
@@ -242,11 +182,6 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max, int wide_min_n
         const int root = b.emit(rest, 0, rest.size());
         a.nodes.reserve(b.tree.size() * BVH_OCTANTS);
         for (int oct = 0; oct < BVH_OCTANTS; oct++) b.thread(root, oct, a.nodes.size());
-        if (b.tree.size() >= (size_t)wide_min_nodes) b.emit4(root, 1);  // only the large-tree builds walk it
-        if (a.depth4 > BVH4_MAX_DEPTH) {  // too deep for the wide walk's fixed stack: the octant walk only
-            a.nodes4.clear();
-            a.depth4 = 0;
-        }
     }
     a.cnodes.reserve(a.nodes.size());
     const size_t per_oct = a.nodes.size() / BVH_OCTANTS;
@@ -265,6 +200,7 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max, int wide_min_n
             c.fr[k] = neg ? lo : hi;
         }
         c.skip = n.skip;
+        for (int k = 0; k < 3; k++) a.bvh_bound = std::max({a.bvh_bound, std::fabs(c.nr[k]), std::fabs(c.fr[k])});
         // a one-shape leaf holds the shape id itself (bit 31), saving the dependent leaf[] load
         if (n.count == 1 && a.leaf[n.first] >= 0 && a.leaf[n.first] < (1 << 24))
             c.first_count = (uint32_t)a.leaf[n.first] | 1u << 24 | 1u << 31;

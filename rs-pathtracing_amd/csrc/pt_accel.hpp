@@ -37,17 +37,13 @@ struct Accel {
     std::vector<int32_t> lin;    // wave-uniform list
     std::vector<int32_t> march;  // ray-marched shapes
     std::vector<DBox> boxes;     // padded world AABB per shape
-    // the same tree collapsed to 4-ary nodes (node 0 the root), for the wide walk; empty when the tree is
-    // empty or deeper than BVH4_MAX_DEPTH
-    std::vector<DNode4> nodes4;
-    int depth4 = 0;
+    float bvh_bound = 0.f;  // >= |every plane of cnodes| (dev::Scene::bvh_bound)
 };
 
 constexpr int LIN_MAX = 32;  // JSON shape count up to which the JSON shapes form `lin`
 
-// leaf_max: shapes per BVH leaf (the renderer option "bvh_leaf"); the wide BVH is built for trees of at
-// least wide_min_nodes binary nodes (tests build it for small trees too)
-Accel build_accel(const Scene &sc, int json_shapes, int leaf_max = 1, int wide_min_nodes = BIG_BVH_NODES);
+// leaf_max: shapes per BVH leaf (the renderer option "bvh_leaf")
+Accel build_accel(const Scene &sc, int json_shapes, int leaf_max = 1);
 // conservative world AABB of one shape (reference get_bounding_box + padding)
 DBox shape_box(const HostShape &s);
 

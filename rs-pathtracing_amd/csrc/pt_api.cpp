@@ -280,8 +280,8 @@ void free_share(GpuShare &g) {
     (void)hipSetDevice(g.device);
     if (g.stream) (void)hipStreamSynchronize(g.stream);
     DeviceScene &d = g.ds;
-    void *bufs[] = {d.shapes, d.mats, d.nodes, d.nodes4, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images,
-                    d.pixels, d.guard};
+    void *bufs[] = {d.shapes, d.mats, d.nodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images, d.pixels,
+                    d.guard};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     d = DeviceScene{};
@@ -306,8 +306,7 @@ struct StagedAccel {
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     int nnodes = 0, nlin = 0, nmarch = 0;
-    DNode4 *nodes4 = nullptr;
-    int nnodes4 = 0;
+    float bvh_bound = 0.f;
 };
 
 // Test hook (renderer option "fault_accel_alloc" = n): the n-th device
@@ -316,7 +315,7 @@ std::atomic<int> g_fault_accel_alloc{0};
 
 void free_staged(int device, StagedAccel &a) {
     (void)hipSetDevice(device);
-    void *bufs[] = {a.nodes, a.leaf, a.lin, a.march, a.boxes, a.nodes4};
+    void *bufs[] = {a.nodes, a.leaf, a.lin, a.march, a.boxes};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     a = StagedAccel{};
@@ -339,7 +338,6 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out) {
     upload(&a.lin, acc.lin);
     upload(&a.march, acc.march);
     upload(&a.boxes, acc.boxes);
-    if (!acc.nodes4.empty()) upload(&a.nodes4, acc.nodes4);
     if (err != hipSuccess) {
         free_staged(device, a);
         return hip_fail(err, "uploading the acceleration structure");
@@ -347,7 +345,7 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out) {
     a.nnodes = acc.nodes_per_octant();  // nodes per octant layout
     a.nlin = (int)acc.lin.size();
     a.nmarch = (int)acc.march.size();
-    a.nnodes4 = (int)acc.nodes4.size();
+    a.bvh_bound = acc.bvh_bound;
     *out = a;
     return PT_OK;
 }
@@ -358,7 +356,7 @@ int commit_accel(GpuShare &g, StagedAccel &a) {
     HIP_TRY(hipSetDevice(g.device));
     HIP_TRY(hipDeviceSynchronize());
     DeviceScene &d = g.ds;
-    StagedAccel old{d.nodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.nodes4, d.nnodes4};
+    StagedAccel old{d.nodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.bvh_bound};
     d.nodes = a.nodes;
     d.leaf = a.leaf;
     d.lin = a.lin;
@@ -367,8 +365,7 @@ int commit_accel(GpuShare &g, StagedAccel &a) {
     d.nnodes = a.nnodes;
     d.nlin = a.nlin;
     d.nmarch = a.nmarch;
-    d.nodes4 = a.nodes4;
-    d.nnodes4 = a.nnodes4;
+    d.bvh_bound = a.bvh_bound;
     a = StagedAccel{};
     free_staged(g.device, old);
     return PT_OK;

@@ -92,6 +92,9 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
               n.x * m[2] + n.y * m[6] + n.z * m[10]);
 }
 
+#ifndef PT_SLAB32
+#define PT_SLAB32 0  // A/B knob: the large-tree builds' BVH slab test in f32 with a conservative widening
+#endif
 #ifndef PT_AXIS_LEAF
 #define PT_AXIS_LEAF 0  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t (A/B knob)
 #endif
@@ -329,6 +332,7 @@ struct Scene {
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
     int nmats;
     int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
+    float bvh_bound;  // >= |every BVH node plane| (the f32 slab's error bound, PT_SLAB32)
     // marches dropped by the march guard (pt_march.hpp MARCH_GUARD), counted
     // on the device (pt_march_guard_drops); null: not counted
     unsigned long long *guard;
@@ -385,84 +389,9 @@ PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first,
     }
 }
 
-// The wide BVH (DNode4, pt_types.hpp; Scene::nodes holds the DNode4 array and
-// nnodes its size in the builds that walk it): each step tests the boxes of a
-// node's (up to four) children together — the near plane of each axis picked by
-// the ray direction's sign bit, t = fma(b, 1/d, -o/d) as in the FMA_SLAB octant
-// walk, so the same conservative argument holds — tests the leaf children's
-// shapes at once, then goes on to the nearest inner child and pushes the others
-// on a per-lane stack (stk[j * stride], at most 3 per level: BVH4_MAX_DEPTH
-// levels fit BVH4_STACK entries).  The hits are decided by the same exact shape
-// tests and tie rule as every other walk, so the result does not depend on the
-// visiting order.  A step is one dependent 128-byte load where the binary walk
-// spends one per visited node (~3.5x as many on C5).
-template <bool STATS = false>
-PT_HD void walk_bvh4(const Scene &sc, const Ray &r, V3 inv, double min_t, double &best, int &who, int32_t *stk,
-                     int stride, Ctr *ct) {
-    const DNode4 *nodes = (const DNode4 *)(const void *)sc.nodes;
-    const bool sx = __builtin_signbit(r.d.x), sy = __builtin_signbit(r.d.y), sz = __builtin_signbit(r.d.z);
-    auto open_inf = [](double m) { return __builtin_isinf(m) ? __builtin_nan("") : m; };
-    const double mx = open_inf(-(r.o.x * inv.x)), my = open_inf(-(r.o.y * inv.y)), mz = open_inf(-(r.o.z * inv.z));
-    const bool axis_ok = PT_AXIS_LEAF && axis_ray_ok(r.o, r.d);
-    int sp = 0, node = 0;
-    for (;;) {
-        const DNode4 &N = nodes[node];
-        PT_LP(BVH_NODE);
-        double tn[4];
-        int hit = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (STATS) ct->c[C_NODE_SLABS]++;
-            const double nx = (double)(sx ? N.hi[0][k] : N.lo[0][k]), fx = (double)(sx ? N.lo[0][k] : N.hi[0][k]);
-            const double ny = (double)(sy ? N.hi[1][k] : N.lo[1][k]), fy = (double)(sy ? N.lo[1][k] : N.hi[1][k]);
-            const double nz = (double)(sz ? N.hi[2][k] : N.lo[2][k]), fz = (double)(sz ? N.lo[2][k] : N.hi[2][k]);
-            const double a = fmax(fmax(__builtin_fma(nx, inv.x, mx), __builtin_fma(ny, inv.y, my)),
-                                  fmax(__builtin_fma(nz, inv.z, mz), min_t));
-            const double b = fmin(fmin(__builtin_fma(fx, inv.x, mx), __builtin_fma(fy, inv.y, my)),
-                                  fmin(__builtin_fma(fz, inv.z, mz), best));
-            tn[k] = a;
-            if (k < N.n && a <= b) hit |= 1 << k;
-        }
-        // leaf children first: their hits shrink `best` before the inner children are kept
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int32_t c = N.child[k];
-            if (((hit >> k) & 1) && c < 0) {
-                PT_LP(BVH_ENTER);
-                const uint32_t u = ~(uint32_t)c;
-                const bool direct = (u >> 24) == 0;
-                bvh_leaf_test<STATS>(sc, r, axis_ok, (int)(u & 0xffffffu), direct ? 1 : (int)(u >> 24), direct,
-                                     min_t, best, who, ct);
-            }
-        }
-        int next = -1;
-        double tmin = __builtin_inf();
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int32_t c = N.child[k];
-            if (((hit >> k) & 1) && c >= 0 && tn[k] <= best) {
-                PT_LP(BVH_ENTER);
-                if (tn[k] < tmin) {
-                    if (next >= 0) stk[(sp++) * stride] = next;
-                    next = c;
-                    tmin = tn[k];
-                } else {
-                    stk[(sp++) * stride] = c;
-                }
-            }
-        }
-        if (next < 0) {
-            if (sp == 0) break;
-            next = stk[(--sp) * stride];
-        }
-        node = next;
-    }
-}
-
-// WIDE: the large-tree builds walk the wide BVH (walk_bvh4) with the caller's stack (stk, stride).
-template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false, bool WIDE = false>
+template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
-                           Ctr *ct = nullptr, bool any = false, int32_t *stk = nullptr, int stride = 0) {
+                           Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
     int who = *who_out;
     // wave-uniform list (few JSON shapes): scalar loads of each shape
@@ -485,12 +414,6 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
             best = t;
             who = i;
         }
-    }
-    if (WIDE) {
-        if (sc.nnodes > 0 && !(any && who >= 0)) walk_bvh4<STATS>(sc, r, inv, min_t, best, who, stk, stride, ct);
-        *best_t = best;
-        *who_out = who;
-        return;
     }
     // threaded BVH over the remaining non-marched shapes, in the layout of the
     // ray's direction octant (near child first, pt_accel.hpp).  The octant is
@@ -520,18 +443,52 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
     auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };
     const bool axis_ok = PT_AXIS_LEAF && axis_ray_ok(r.o, r.d);
+    // SLAB32 (PT_SLAB32, the FMA_SLAB builds): the planes' t in f32, t = fma(b, 1/d, -o/d), widened on each
+    // axis by e = 2^-21 (B + |o|) |1/d| (B >= every plane's |b|): against the real t = (b - o) / d, the f32
+    // 1/d and -o/d (each 2^-24 relative, after the f64 rounding), the fma's rounding and the widening's own
+    // rounding add up to less than 1.6 * 2^-23 (|b| + |o|) |1/d|, so the widened interval contains the real
+    // one and the cull stays conservative (1e-30 more covers an f32 flush of tiny values).  An axis whose
+    // 1/d or -o/d does not fit an f32 is left open (NaN t's drop out of fmax/fmin); min_t is rounded down and
+    // best up.  The hits are decided by the exact f64 leaf tests as in every walk.
+    constexpr bool S32 = FMA_SLAB && PT_SLAB32;
+    auto axis32 = [&](double o, double iv, float *i32, float *m32, float *e32) {
+        const double m = -(o * iv);
+        const bool fits = fabs(iv) < 1e30 && fabs(m) < 1e30;
+        *i32 = (float)iv;
+        *m32 = fits ? (float)m : __builtin_nanf("");
+        *e32 = (float)((0x1p-21 * (1.0 + 0x1p-20)) * ((double)sc.bvh_bound + fabs(o)) * fabs(iv) + 1e-30);
+    };
+    float ix = 0.f, iy = 0.f, iz = 0.f, mx32 = 0.f, my32 = 0.f, mz32 = 0.f, ex = 0.f, ey = 0.f, ez = 0.f;
+    if (S32) {
+        axis32(r.o.x, inv.x, &ix, &mx32, &ex);
+        axis32(r.o.y, inv.y, &iy, &my32, &ey);
+        axis32(r.o.z, inv.z, &iz, &mz32, &ez);
+    }
+    const float mt32 = S32 ? (float)(min_t - fabs(min_t) * 0x1p-20) : 0.f;
+    float best32 = S32 ? (float)(best + fabs(best) * 0x1p-20) : 0.f;
     int n = any && who >= 0 ? sc.nnodes : 0;
     while (n < sc.nnodes) {
         const DNodeC nd = nodes[n];
         PT_LP(BVH_NODE);
         if (STATS) ct->c[C_NODE_SLABS]++;
-        const double tn = fmax(fmax(tx(nd.nr[0]), ty(nd.nr[1])), fmax(tz(nd.nr[2]), min_t));
-        const double tf = fmin(fmin(tx(nd.fr[0]), ty(nd.fr[1])), fmin(tz(nd.fr[2]), best));
-        if (tn <= tf) {
+        bool enter;
+        if (S32) {
+            const float tn = fmaxf(fmaxf(__builtin_fmaf(nd.nr[0], ix, mx32) - ex, __builtin_fmaf(nd.nr[1], iy, my32) - ey),
+                                   fmaxf(__builtin_fmaf(nd.nr[2], iz, mz32) - ez, mt32));
+            const float tf = fminf(fminf(__builtin_fmaf(nd.fr[0], ix, mx32) + ex, __builtin_fmaf(nd.fr[1], iy, my32) + ey),
+                                   fminf(__builtin_fmaf(nd.fr[2], iz, mz32) + ez, best32));
+            enter = tn <= tf;
+        } else {
+            const double tn = fmax(fmax(tx(nd.nr[0]), ty(nd.nr[1])), fmax(tz(nd.nr[2]), min_t));
+            const double tf = fmin(fmin(tx(nd.fr[0]), ty(nd.fr[1])), fmin(tz(nd.fr[2]), best));
+            enter = tn <= tf;
+        }
+        if (enter) {
             PT_LP(BVH_ENTER);
             const int first = (int)(nd.first_count & 0xffffffu), count = (int)(nd.first_count >> 24 & 0x7fu);
             const bool direct = nd.first_count >> 31;  // one-shape leaf: `first` is the shape id
             bvh_leaf_test<STATS>(sc, r, axis_ok, first, count, direct, min_t, best, who, ct);
+            if (S32) best32 = (float)(best + fabs(best) * 0x1p-20);
             n++;
         } else {
             n = nd.skip;
@@ -760,67 +717,6 @@ PT_HD V3 random_in_unit_sphere(Rng &rng, double s11, Ctr *ct = nullptr) {
 #endif
     }
 }
-// Whether a hit's shade draws random_in_unit_sphere: Lambertian, or Metal with fuzz != 0 (material.rs:41-76).
-PT_HD bool needs_rius(const Scene &sc, int who, uint32_t depth) {
-    if (who < 0 || depth == 0) return false;
-    const DMaterial &m = sc.mats[sc.shapes[who].material];
-    return m.type == LAMBERTIAN || (m.type == METAL && m.fuzz != 0.0);
-}
-
-// random_in_unit_sphere for every lane of the wave that needs it, with the
-// wave's idle lanes drawing the pending lanes' later tries.  The stream is
-// counter based (try k of a lane reads the draws at s + (3k+1..3k+3) GAMMA),
-// so any lane can evaluate any try.  Round by round, each of the p pending
-// lanes gets g = 64 / p helper lanes, which evaluate its tries K .. K+g-1 (every
-// earlier try of every pending lane was rejected); the lowest accepted one is
-// the lane's first accepted try, as the loop would find it.  The lane's rng ends
-// past the draws of that try, as after the loop.  About 3 rounds per wave
-// instead of the loop's ~5.5 trips at ~16 lanes (scripts/bounce_lanes.py).
-// Every lane of the wave must call it (converged); lanes with need == false
-// only help.
-__device__ __forceinline__ V3 coop_rius(bool need, Rng &rng, double s11) {
-    __shared__ uint32_t slot_lane[256];  // per wave: rank of a pending lane -> its lane
-    uint32_t *map = slot_lane + (threadIdx.x & ~63u);
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    uint64_t P = __ballot(need);
-    const uint64_t s0 = rng.s;
-    V3 res = v3(0.0, 0.0, 0.0);
-    uint32_t K = 0;
-    while (P) {
-        const uint32_t p = (uint32_t)__popcll(P);
-        const uint32_t g = 64u / p;
-        const bool pending = (P >> lane) & 1ull;
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(P >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)P, 0u));
-        if (pending) map[rank] = lane;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t q = lane / g, sub = lane % g;
-        const bool helps = q < p;
-        const uint32_t src = map[helps ? q : 0];
-        __builtin_amdgcn_wave_barrier();
-        // the source lane's stream, positioned before its try K + sub
-        const uint32_t lo = __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)s0);
-        const uint32_t hi = __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)(uint32_t)(s0 >> 32));
-        Rng r{(((uint64_t)hi << 32) | lo) + (uint64_t)(3u * (K + sub)) * GAMMA};
-        const double x = r.uniform(-1.0, s11);
-        const double y = r.uniform(-1.0, s11);
-        const double z = r.uniform(-1.0, s11);
-        const bool acc = helps && x * x + y * y + z * z <= 1.0;
-        const uint64_t A = __ballot(acc);
-        // a pending lane's helpers are lanes rank*g .. rank*g+g-1, tries K .. K+g-1 in order
-        const uint64_t mask = g >= 64u ? ~0ull : ((1ull << g) - 1ull);
-        const uint64_t bits = pending ? (A >> (rank * g)) & mask : 0ull;
-        const uint32_t win = bits ? rank * g + (uint32_t)__builtin_ctzll(bits) : lane;
-        const double wx = __shfl(x, (int)win), wy = __shfl(y, (int)win), wz = __shfl(z, (int)win);
-        if (bits) {
-            res = v3(wx, wy, wz);
-            rng.s = s0 + (uint64_t)(3u * (K + (win - rank * g) + 1u)) * GAMMA;
-        }
-        P &= ~__ballot(bits != 0ull);
-        K += g;
-    }
-    return res;
-}
-
 PT_HD V3 reflect(V3 d, V3 n) {  // algebra/mod.rs:122-125
     V3 b = scale(n, dot(d, n));
     return sub(d, scale(b, 2.0));
@@ -888,12 +784,9 @@ struct IdStack {
 // or the wavefront engine's per-slot id array in HBM).
 // EXT: the build for scenes with non-solid textures or a Torus (textured albedos are
 // evaluated at the hit and pushed by value; textured lights emit their value).
-// presample: random_in_unit_sphere's result drawn beforehand for this hit (wf_bounce's wave-cooperative
-// sampler, coop_rius): a Lambertian or fuzzy Metal hit takes it instead of drawing (its rng already advanced
-// past the draws), the draw order being the same.
 template <bool STATS = false, int FK = march::F_ANY, bool EXT = false, class Stack>
 PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, Stack &stk, Rng &rng,
-                 double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr, const V3 *presample = nullptr) {
+                 double s11, V3 *leaf, Ctr *ct = nullptr, uint64_t *tfin = nullptr) {
     if (who < 0) {
         *leaf = background(ray.d);
         return true;
@@ -918,7 +811,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
     if (m.type == LAMBERTIAN) {  // material.rs:41-54
         PT_LP(LAMBERT);
         if (STATS) ct->c[C_LAMBERT]++;
-        V3 u = normalize(presample ? *presample : random_in_unit_sphere<STATS>(rng, s11, ct));
+        V3 u = normalize(random_in_unit_sphere<STATS>(rng, s11, ct));
         dir = add(h.n, u);
         if (approx_zero(dir.x) && approx_zero(dir.y) && approx_zero(dir.z)) dir = h.n;
         if (EXT && m.tex >= 0) stk.push_val(textured());
@@ -927,7 +820,7 @@ PT_HD bool shade(const Scene &sc, int who, double t, Ray &ray, uint32_t &depth, 
         PT_LP(METAL);
         if (STATS) ct->c[C_METAL]++;
         V3 rf = reflect(ray.d, h.n);
-        dir = m.fuzz == 0.0 ? rf : add(rf, scale(presample ? *presample : random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
+        dir = m.fuzz == 0.0 ? rf : add(rf, scale(random_in_unit_sphere<STATS>(rng, s11, ct), m.fuzz));
         if (EXT && m.tex >= 0) stk.push_val(textured());
         else stk.push((uint32_t)s.material);
     } else if (m.type == DIELECTRIC) {  // :92-115

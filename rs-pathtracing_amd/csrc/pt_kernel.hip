@@ -245,6 +245,7 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.pixels = s.pixels;
     d.ext = s.ext;
     d.nnodes = s.nnodes;
+    d.bvh_bound = s.bvh_bound;
     d.nlin = s.nlin;
     d.nmarch = s.nmarch;
     d.nmats = s.nmats;
@@ -376,11 +377,7 @@ static bool use_wavefront(const DeviceScene &s, const FrameParams &P, WaveWorksp
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
                          WaveWorkspace *ws) {
     if (P.tile_count == 0) return hipSuccess;
-    if (use_wavefront(s, P, ws)) {
-        ws->nodes4 = s.nodes4;
-        ws->nnodes4 = s.nnodes4;
-        return launch_render_wave(dscene(s), P, out, st, ws, s.fkind);
-    }
+    if (use_wavefront(s, P, ws)) return launch_render_wave(dscene(s), P, out, st, ws, s.fkind);
     KernelTimer *tm = ws ? ws->timer : nullptr;
     hipError_t e0 = timer_begin(tm, st, K_MEGA);
     if (e0 != hipSuccess) return e0;

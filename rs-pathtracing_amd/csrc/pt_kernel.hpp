@@ -11,14 +11,14 @@ struct DeviceScene {
     DShape *shapes = nullptr;
     DMaterial *mats = nullptr;
     DNodeC *nodes = nullptr;
-    DNode4 *nodes4 = nullptr;  // the wide BVH (large trees; null when not built)
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     DTexture *tex = nullptr;  // non-solid textures (null when the scene has none)
     DPerlin *perlin = nullptr;
     DImage *images = nullptr;
     uint8_t *pixels = nullptr;
-    int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0, nnodes4 = 0;
+    int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
+    float bvh_bound = 0.f;  // Accel::bvh_bound
     int ext = 0;    // non-solid textures or a Torus: the extended (EXT) kernel builds
     int fkind = 0;  // 0: every marched shape is a Heart (or none) -> Heart-only kernel builds; -1: any
     int diag = 0;  // Tuning::diag (timing ablation), copied here for the probes
@@ -81,9 +81,6 @@ struct WaveWorkspace {
     bool used = false;
     int device = -1;
     int side_priority = 0;  // the priority the side streams were created with (Tuning::wf_side_priority)
-    // the scene's wide BVH for this frame (launch_render sets them; the bounce's large-tree build walks it)
-    const DNode4 *nodes4 = nullptr;
-    int nnodes4 = 0;
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

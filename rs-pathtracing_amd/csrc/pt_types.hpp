@@ -83,23 +83,7 @@ struct alignas(32) DNodeC {
 };
 static_assert(sizeof(DNodeC) == 32, "DNodeC is half a cache line");
 
-// Wide (4-ary) BVH node for large trees (C5: 100k spheres), one 128-byte line:
-// the boxes of up to four children, f32 rounded outward like DNodeC's, stored
-// per axis plane (lo[axis][child], hi[axis][child]: one 16-byte load reads a
-// plane of all four), and the children: child >= 0 an inner node; child < 0 a
-// leaf c = ~child, holding shape c itself when c < 2^24, else c >> 24 shapes
-// from leaf[c & 0xffffff].  The walk (dev::walk_bvh4) tests the four boxes of
-// a node together and keeps the pending children on a per-lane stack.
-struct alignas(128) DNode4 {
-    float lo[3][4], hi[3][4];
-    int32_t child[4];
-    int32_t n;  // children in use (1..4); the others never match
-    int32_t pad[3];
-};
-static_assert(sizeof(DNode4) == 128, "DNode4 is one 128-byte line");
 constexpr int BIG_BVH_NODES = 1 << 15;  // binary nodes from which the bounce runs its large-tree builds (C5)
-constexpr int BVH4_STACK = 32;      // stack entries per lane (dev::walk_bvh4)
-constexpr int BVH4_MAX_DEPTH = 10;  // a tree deeper than this keeps the octant walk (3 pushes per level fit)
 
 struct DBox {
     double lo[3], hi[3];

@@ -277,15 +277,10 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // points along a march job's chord whose sign of f predicts a hit (queue
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
 constexpr int WF_PREDICT = 4;
-#ifndef PT_BVH4
-#define PT_BVH4 0  // A/B knob: the large-tree bounce build walks the wide BVH (dev::walk_bvh4)
+#ifndef PT_SOA_OPAQUE
+#define PT_SOA_OPAQUE 0  // A/B knob: path-state addresses formed per iteration (scalar) instead of spilled
 #endif
-#ifndef PT_COOP_RIUS
-#define PT_COOP_RIUS 0  // A/B knob: random_in_unit_sphere drawn wave-cooperatively before the shade (dev::coop_rius)
-#endif
-#ifndef PT_LIST_PREFETCH
-#define PT_LIST_PREFETCH 0  // A/B knob: the bounce's next live-list entry loaded one grid-stride iteration ahead
-#endif
+
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
 #endif
@@ -296,11 +291,9 @@ constexpr int WF_PREDICT = 4;
 // only): list load, state loads, shade, unwind, trace, march pre-check,
 // stores; summed into diag[36..42].
 template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false,
-          bool BIGBVH = false, bool WIDE = false>
+          bool BIGBVH = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
                                                         unsigned long long *diag = nullptr) {
-    // WIDE: sc.nodes is the wide BVH (DNode4); each lane's walk stack, entry j at [j * 256 + thread]
-    __shared__ int32_t bvh4_stack[WIDE ? BVH4_STACK * 256 : 1];
     // input: the id-sorted list of live paths (iteration 0: every slot)
     const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -335,20 +328,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         tst = n_;                                                   \
     }
 #endif
-    // (PT_LIST_PREFETCH) the next grid-stride iteration's live-list entry is loaded one iteration ahead, so
-    // each iteration starts with one dependent round trip (the state) instead of two (list, then state)
-    uint32_t p_next = 0;
-    if (PT_LIST_PREFETCH && !FIRST && blockIdx.x * blockDim.x + threadIdx.x < count)
-        p_next = v.list[blockIdx.x * blockDim.x + threadIdx.x];
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         if (DIAG) tst = __builtin_amdgcn_s_memtime();
         const uint32_t i = base + threadIdx.x;
         bool live = i < count;
-        uint32_t p_cur = 0;
-        if (PT_LIST_PREFETCH && !FIRST) {
-            p_cur = p_next;
-            if (i + stride < count) p_next = v.list[i + stride];
-        }
         uint32_t id = 0;
         Ray ray;
         dev::Rng rng{0};
@@ -372,9 +355,12 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                     if (EXT) stk.vb = v.att + id;
                 }
             } else {
-                const uint32_t p = PT_LIST_PREFETCH ? p_cur : v.list[i];
+                const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
-                const PathSoA &S = v.in;
+                PathSoA S = v.in;
+                // (PT_SOA_OPAQUE) the set's size made opaque here, so its 11 array addresses are formed per
+                // iteration with scalar ops rather than held across the loop in spilled SGPRs (v_readlane)
+                if (PT_SOA_OPAQUE) asm volatile("" : "+s"(S.cap));
                 id = ld_path(S.sid() + p);
                 ray.o = dev::v3(ld_path(S.ox() + p), ld_path(S.oy() + p), ld_path(S.oz() + p));
                 ray.d = dev::v3(ld_path(S.dx() + p), ld_path(S.dy() + p), ld_path(S.dz() + p));
@@ -394,16 +380,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         // starts before its best hit.  (Up to 2-3 bounces per launch for paths
         // needing no march measured +0.8 % / -2.5 %, round 2.)
         bool need_march = false, long_job = false;
-        V3 pre = dev::v3(0.0, 0.0, 0.0);
-        if (PT_COOP_RIUS && !FIRST && !EXT)  // converged: every lane of the wave takes part
-            pre = dev::coop_rius(live && dev::needs_rius(sc, who, depth), rng, P.s11);
         if (live) {
             PT_LP(LIVE);
             if (!FIRST) {
                 V3 leaf;
-                const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf,
-                                                              nullptr, nullptr,
-                                                              PT_COOP_RIUS && !EXT ? &pre : nullptr);
+                const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
                 PT_BSTAMP(2)
                 if (ended) {
                     // the leaf radiance and the stack depth; wf_reduce unwinds
@@ -424,8 +405,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             // miss matters (any hit gives black), so a path with a hit found
             // needs no march either
             const bool any = depth == 0;
-            dev::closest_nomarch<false, EXT, BIGBVH, WIDE>(sc, ray, inv, T_MIN, &best, &who, nullptr, any,
-                                                           bvh4_stack + threadIdx.x, 256);
+            dev::closest_nomarch<false, EXT, BIGBVH>(sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
             // march kernel marches it)
@@ -477,7 +457,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         // every input position's state is written (ended paths too: whole lines; storeab)
         if (i < count) PT_LP(STORE);
         if (i < count)
-            store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+        {
+            PathSoA O = v.out;
+            if (PT_SOA_OPAQUE) asm volatile("" : "+s"(O.cap));
+            store_path(O, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+        }
         if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
     }
@@ -1195,8 +1179,7 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
 // (dev::closest_nomarch): C5's 100k-sphere tree has ~200k, cornell's ~960.
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
-                          const WfView &v, int it, unsigned long long *diag, int fkind, int waves,
-                          const DNode4 *nodes4 = nullptr, int nnodes4 = 0) {
+                          const WfView &v, int it, unsigned long long *diag, int fkind, int waves) {
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
         wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
@@ -1214,13 +1197,6 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
         return;
     }
     if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH (C5): the FMA slab build
-        if (PT_BVH4 && nodes4 && nnodes4 > 0) {  // ... walking the wide BVH
-            dev::Scene w = sc;
-            w.nodes = (const DNodeC *)(const void *)nodes4;
-            w.nnodes = nnodes4;
-            wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true, true><<<blocks, 256, 0, st>>>(w, P, v, it);
-            return;
-        }
         wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
         return;
     }
@@ -1487,12 +1463,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
                 if (it == 0) {
                     if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves,
-                                                 ws->nodes4, ws->nnodes4);
+                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves);
                 } else {
                     if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind, tu.wf_bounce_waves,
-                                                  ws->nodes4, ws->nnodes4);
+                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind, tu.wf_bounce_waves);
                 }
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;

@@ -25,7 +25,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
     try {
         Bundle *b = new Bundle();  // value-initialised: every dev::Scene field not set below is 0 (cancel: none)
         b->sc = scene_from_json(json, len, random_spheres != 0, seed);
-        b->acc = build_accel(b->sc, b->sc.json_shapes, 1, 0);  // with the wide BVH, whatever the tree's size
+        b->acc = build_accel(b->sc, b->sc.json_shapes);
         for (auto &s : b->sc.shapes) b->shapes.push_back(to_device(s));
         for (auto &m : b->sc.materials) b->mats.push_back(to_device(m));
         b->view.shapes = b->shapes.data();
@@ -41,6 +41,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.images = tex ? b->sc.images.data() : nullptr;
         b->view.pixels = tex ? b->sc.pixels.data() : nullptr;
         b->view.nnodes = b->acc.nodes_per_octant();
+        b->view.bvh_bound = b->acc.bvh_bound;
         b->view.nlin = (int)b->acc.lin.size();
         b->view.nmarch = (int)b->acc.march.size();
         b->view.diag = 0;
@@ -53,8 +54,6 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
 extern "C" void h_scene_free(void *p) { delete (Bundle *)p; }
 extern "C" void h_accel_stats(void *p, int *out) {
     Bundle *b = (Bundle *)p;
-    out[4] = (int)b->acc.nodes4.size();
-    out[5] = b->acc.depth4;
     out[0] = b->acc.nodes_per_octant();
     out[1] = (int)b->acc.lin.size();
     out[2] = (int)b->acc.march.size();
@@ -170,8 +169,7 @@ extern "C" void h_count_work(void *p, uint32_t w, uint32_t h, uint32_t spp, uint
 
 // The non-marched closest hit (uniform list + BVH) with the BVH slab in one of
 // its two arithmetic forms: fma = 0 (b - o) * 1/d, 1 fma(b, 1/d, -o/d) (the
-// FMA_SLAB bounce build for large BVHs); fma = 2: the wide (4-ary) BVH walk of
-// the large-tree builds.  All must give the same (who, t).
+// FMA_SLAB bounce build for large BVHs).  Both must give the same (who, t).
 extern "C" int h_closest_nomarch(void *p, const double *ray, int fma, double *t) {
     Bundle *b = (Bundle *)p;
     dev::Ray r;
@@ -180,13 +178,7 @@ extern "C" int h_closest_nomarch(void *p, const double *ray, int fma, double *t)
     const dev::V3 inv = dev::v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
     double best = __builtin_inf();
     int who = -1;
-    if (fma == 2) {  // the wide BVH walk (DNode4) with a host stack
-        dev::Scene w = b->view;
-        w.nodes = (const DNodeC *)(const void *)b->acc.nodes4.data();
-        w.nnodes = (int)b->acc.nodes4.size();
-        int32_t stk[BVH4_STACK];
-        dev::closest_nomarch<false, false, true, true>(w, r, inv, T_MIN, &best, &who, nullptr, false, stk, 1);
-    } else if (fma) {
+    if (fma) {
         dev::closest_nomarch<false, false, true>(b->view, r, inv, T_MIN, &best, &who);
     } else {
         dev::closest_nomarch<false, false, false>(b->view, r, inv, T_MIN, &best, &who);

@@ -103,6 +103,13 @@ __device__ __forceinline__ void lit_begin() { begin(R_LIT); }
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
 
+#ifndef PT_LEAF_AOS
+#define PT_LEAF_AOS 0  // A/B knob: an ended path's leaf radiance and depth as one 32-byte record per slot
+#endif
+#ifndef PT_SOA_OPAQUE
+#define PT_SOA_OPAQUE 0  // A/B knob: path-state addresses formed per iteration (scalar) instead of spilled
+#endif
+
 namespace pt {
 
 using dev::Ray;
@@ -224,7 +231,16 @@ __device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3
 // (the recursion's products, in its order) when it sums the chunk's samples,
 // so the bounce kernel's waves never wait for the unwind's dependent loads.
 // Non-temporal (read once, by the chunk's reduce): iso bounce -0.6 ms, C2 +0.4 %.
+// (PT_LEAF_AOS) the leaf and the depth as one 32-byte record per slot at v.rx (two 16-byte stores): an ended
+// path's write touches one line instead of four (rx, ry, rz, fin), and only ~1 lane in 8 ends per bounce.
 __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const MemStack &stk, V3 leaf) {
+    if (PT_LEAF_AOS) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        d2v *rec = (d2v *)(v.rx + (size_t)id * 4);
+        __builtin_nontemporal_store((d2v){leaf.x, leaf.y}, rec);
+        __builtin_nontemporal_store((d2v){leaf.z, __builtin_bit_cast(double, (uint64_t)(uint32_t)stk.n)}, rec + 1);
+        return;
+    }
     __builtin_nontemporal_store(leaf.x, v.rx + id);
     __builtin_nontemporal_store(leaf.y, v.ry + id);
     __builtin_nontemporal_store(leaf.z, v.rz + id);
@@ -277,9 +293,6 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // points along a march job's chord whose sign of f predicts a hit (queue
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
 constexpr int WF_PREDICT = 4;
-#ifndef PT_SOA_OPAQUE
-#define PT_SOA_OPAQUE 0  // A/B knob: path-state addresses formed per iteration (scalar) instead of spilled
-#endif
 
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
@@ -1064,8 +1077,15 @@ __global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, W
     V3 a = first ? dev::v3(0.0, 0.0, 0.0) : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
     for (uint32_t s = 0; s < v.ns; s++) {
         const size_t id = (size_t)s * v.npix + pl;
-        MemStack stk{v.ids + id, (size_t)v.cap, (int)v.fin[id], EXT ? v.att + id : nullptr};
-        a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(v.rx[id], v.ry[id], v.rz[id])));
+        if (PT_LEAF_AOS) {
+            const double *rec = v.rx + id * 4;
+            const uint32_t fin = (uint32_t)__builtin_bit_cast(uint64_t, rec[3]);
+            MemStack stk{v.ids + id, (size_t)v.cap, (int)fin, EXT ? v.att + id : nullptr};
+            a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(rec[0], rec[1], rec[2])));
+        } else {
+            MemStack stk{v.ids + id, (size_t)v.cap, (int)v.fin[id], EXT ? v.att + id : nullptr};
+            a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(v.rx[id], v.ry[id], v.rz[id])));
+        }
     }
     if (last) {
         const V3 c = dev::divs(a, (double)P.spp);
@@ -1367,9 +1387,14 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         }
         v.fin = (uint32_t *)take((size_t)cap * 4);
         v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
-        v.rx = (double *)take((size_t)cap * 8);
-        v.ry = (double *)take((size_t)cap * 8);
-        v.rz = (double *)take((size_t)cap * 8);
+        if (PT_LEAF_AOS) {
+            v.rx = (double *)take((size_t)cap * 32);  // 32-byte leaf records (end_path)
+            v.ry = v.rz = nullptr;
+        } else {
+            v.rx = (double *)take((size_t)cap * 8);
+            v.ry = (double *)take((size_t)cap * 8);
+            v.rz = (double *)take((size_t)cap * 8);
+        }
         v.list = (uint32_t *)take((size_t)cap * 4);
         v.mq = (uint32_t *)take((size_t)cap * 4);
         v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);

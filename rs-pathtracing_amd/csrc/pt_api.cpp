@@ -399,7 +399,7 @@ int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const 
     StagedAccel a;
     if (int rc = stage_accel(device, acc, &a)) return rc;
     if (int rc = commit_accel(g, a)) return rc;
-    g.ws.tune = tuning_from_env();
+    g.ws.tune = tuning_defaults();
     g.ds.diag = g.ws.tune.diag;
     g.ds.nshapes = (int)hs.size();
     g.ds.nmats = (int)hm.size();
@@ -602,7 +602,7 @@ int create_renderer(pt_scene *scene, const std::vector<int> &devices, uint32_t d
         for (auto &s : scene->s.shapes) hs.push_back(to_device(s));
         for (auto &m : scene->s.materials) hm.push_back(to_device(m));
         if (hm.empty()) hm.push_back(DMaterial{});
-        const Accel acc = build_accel(scene->s, scene->s.json_shapes, tuning_from_env().bvh_leaf);
+        const Accel acc = build_accel(scene->s, scene->s.json_shapes, tuning_defaults().bvh_leaf);
         r->gpus.resize(devices.size());
         for (size_t k = 0; k < devices.size(); k++) {
             if (int rc = init_share(r->gpus[k], devices[k], scene->s, acc, hs, hm)) {

@@ -712,9 +712,6 @@ PT_HD V3 random_in_unit_sphere(Rng &rng, double s11, Ctr *ct = nullptr) {
         double y = rng.uniform(-1.0, s11);
         double z = rng.uniform(-1.0, s11);
         if (x * x + y * y + z * z <= 1.0) return v3(x, y, z);
-#ifdef PT_ABL_ONETRY
-        return v3(x * 0.5, y * 0.5, z * 0.5);  // timing ablation only (not exact): no rejection loop
-#endif
     }
 }
 PT_HD V3 reflect(V3 d, V3 n) {  // algebra/mod.rs:122-125

@@ -338,21 +338,7 @@ int tuning_get(const Tuning &t0, const char *name, int64_t *v) {
     return PT_OK;
 }
 
-Tuning tuning_from_env() {
-    Tuning t;
-    static const struct {
-        const char *env, *name;
-    } map[] = {{"PT_WAVES", "mega_waves"}, {"PT_DIAG", "diag"}, {"PT_WF_SLOTS", "wf_slots"},
-               {"PT_WF_PATHS", "wf_paths"}, {"PT_WF_MIN_CHUNKS", "wf_min_chunks"},
-               {"PT_WF_BOUNCE_WAVES", "wf_bounce_waves"}, {"PT_WF_FUSED", "wf_fused"},
-               {"PT_WF_MARCH_SLICE", "wf_march_slice"}, {"PT_WF_TRACE_SLICE", "wf_trace_slice"},
-               {"PT_WF_MARCH_BLOCKS_PER_CU", "wf_march_blocks_per_cu"}, {"PT_WF_SIDE_PRIORITY", "wf_side_priority"},
-               {"PT_WF_PINGPONG", "wf_pingpong"}, {"PT_BVH_LEAF", "bvh_leaf"}};
-    for (const auto &m : map)
-        if (const char *e = getenv(m.env)) (void)tuning_set(&t, m.name, atoll(e));  // out of range: default kept
-    if (const char *e = getenv("PT_ENGINE")) t.engine = e[0] == 'm' ? 1 : (e[0] == 'w' ? 2 : 0);
-    return t;
-}
+Tuning tuning_defaults() { return Tuning{}; }
 
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
                               WaveWorkspace *ws, int fkind);

@@ -37,27 +37,26 @@ hipError_t timer_begin(KernelTimer *t, hipStream_t st, int kind);  // no-op when
 hipError_t timer_end(KernelTimer *t, hipStream_t st);
 hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches);  // sums since last collect
 
-// Tuning knobs of the render engines (pt_renderer_set_option).  The defaults
-// are the measured optimum on MI355X.  A renderer takes its
-// initial values from the PT_* environment variables named below, once, when
-// it is created; bench.py reports every knob that differs from its default.
+// Tuning knobs of the render engines (pt_renderer_set_option; the option names
+// are the field names).  The defaults are the measured optimum on MI355X
+// (DESIGN.md §5); bench.py reports every knob that differs from its default.
 struct Tuning {
-    int engine = 0;                  // PT_ENGINE: 0 auto (wavefront for a scene that marches or has textures / a Torus, and for any frame of >= 2^22 samples; else the megakernel), 1 megakernel, 2 wavefront
-    int mega_waves = 4;              // PT_WAVES: megakernel register budget, waves per SIMD (2..5)
-    int diag = 0;                    // PT_DIAG bit 0: skip ray-marched shapes (a timing ablation, not the reference)
-    int wf_slots = 2;                // PT_WF_SLOTS: sample chunks in flight, one stream each (1..4)
-    int64_t wf_paths = 3 << 24;      // PT_WF_PATHS: path slots per chunk (256 .. 2^28); 48M: 24 spp of 1080p (24M: 1795, 32M: 1818, 48M: 1830, 64M: 1832 M samples/s)
-    int wf_min_chunks = 1;           // PT_WF_MIN_CHUNKS: at least this many sample chunks per frame (1..4096)
-    int wf_bounce_waves = 3;         // PT_WF_BOUNCE_WAVES: wf_bounce register budget (2, 3, 4, 5, 6, 8)
-    int wf_fused = 0;                // PT_WF_FUSED: fused bounces (wf_trace) instead of one launch per bounce
-    int wf_march_slice = 256;        // PT_WF_MARCH_SLICE: march-queue run dealt to a block (0 = contiguous share)
-    int wf_trace_slice = 256;        // PT_WF_TRACE_SLICE: live-list run dealt to a wf_trace block
-    int wf_march_blocks_per_cu = 0;  // PT_WF_MARCH_BLOCKS_PER_CU: persistent march grid (0 = occupancy maximum)
-    int wf_side_priority = 0;        // PT_WF_SIDE_PRIORITY: the library's chunk streams' priority (-1 low, 0 normal, 1 high)
-    int wf_pingpong = 0;             // PT_WF_PINGPONG: bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
-    int bvh_leaf = 1;                // PT_BVH_LEAF: shapes per BVH leaf (1..16; C5 677 / 609 / 534 M samples/s at 1 / 2 / 4)
+    int engine = 0;                  // 0 auto (wavefront for a scene that marches or has textures / a Torus, and for any frame of >= 2^22 samples; else the megakernel), 1 megakernel, 2 wavefront
+    int mega_waves = 4;              // megakernel register budget, waves per SIMD (2..5)
+    int diag = 0;                    // bit 0: skip ray-marched shapes (a timing ablation, not the reference)
+    int wf_slots = 2;                // sample chunks in flight, one stream each (1..4)
+    int64_t wf_paths = 3 << 24;      // path slots per chunk (256 .. 2^28); 48M: 24 spp of 1080p (24M: 1795, 32M: 1818, 48M: 1830, 64M: 1832 M samples/s)
+    int wf_min_chunks = 1;           // at least this many sample chunks per frame (1..4096)
+    int wf_bounce_waves = 3;         // wf_bounce register budget (2, 3, 4, 5, 6, 8)
+    int wf_fused = 0;                // fused bounces (wf_trace) instead of one launch per bounce
+    int wf_march_slice = 256;        // march-queue run dealt to a block (0 = contiguous share)
+    int wf_trace_slice = 256;        // live-list run dealt to a wf_trace block
+    int wf_march_blocks_per_cu = 0;  // persistent march grid (0 = occupancy maximum)
+    int wf_side_priority = 0;        // the library's chunk streams' priority (-1 low, 0 normal, 1 high)
+    int wf_pingpong = 0;             // bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
+    int bvh_leaf = 1;                // shapes per BVH leaf (1..16; C5 677 / 609 / 534 M samples/s at 1 / 2 / 4)
 };
-Tuning tuning_from_env();
+Tuning tuning_defaults();  // the measured defaults; a renderer changes them only through pt_renderer_set_option
 // 0 on success, PT_ERR_INVALID for an unknown name or a value out of range
 int tuning_set(Tuning *t, const char *name, int64_t value);
 int tuning_get(const Tuning &t, const char *name, int64_t *value);
@@ -85,8 +84,8 @@ struct WaveWorkspace {
 void wave_workspace_free(WaveWorkspace *ws);
 
 // Renders this rank's tiles of P into out.  Scenes with ray-marched shapes use
-// the wavefront engine (ws required), others the megakernel; PT_ENGINE=mega or
-// PT_ENGINE=wave in the environment forces one.
+// the wavefront engine (ws required), others the megakernel; the renderer
+// option "engine" (1 megakernel, 2 wavefront) forces one.
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
                          WaveWorkspace *ws);
 // rows [y0, y1) of the frame from gathered shards (pt_unshard_device)

@@ -39,66 +39,7 @@
 #include <cstdlib>
 #include <vector>
 
-#ifdef PT_MARCH_REGIONS
-// Tuning builds only: wave wall-clock (s_memtime) spent in each region of
-// the march kernel (pt_march.hpp's PT_MREG points), as seen by the wave's
-// first active lane, summed over all waves, the same weighted by the lanes
-// active at the region's start, and per profiling point of pt_march.hpp
-// (PT_MPROF: one per segment, halving level, literal add, ...) the wave
-// passes and the lanes active in them (pt_march_regions).
-namespace pt {
-namespace mreg {
-enum { R_ITER, R_POLY, R_PREFIX, R_HALVE, R_ADV, R_LIT, R_REFILL, R_TOTAL, R_N };
-enum { P_iters, P_lin_init, P_lit_adds, P_advance_loops, P_evals, P_sir_inside, P_lin_fail_zero, P_lin_fail_q,
-       P_lin_fail_tie, P_lin_fail_zone, P_N };
-constexpr int G_N = 2 * R_N + 2 * P_N;
-__device__ unsigned long long g_acc[G_N];
-__shared__ unsigned long long t0[4][R_N], acc[4][R_N], accl[4][R_N], n0[4][R_N], pw[4][P_N], pl[4][P_N];
-__device__ __forceinline__ unsigned long long now() {
-    __builtin_amdgcn_sched_barrier(0);
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-__device__ __forceinline__ bool leader() {
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    return lane == (uint32_t)__builtin_ctzll(__ballot(1));
-}
-__device__ __forceinline__ void begin(int r) {
-    const unsigned long long m = __ballot(1);
-    if (leader()) {
-        t0[threadIdx.x >> 6][r] = now();
-        n0[threadIdx.x >> 6][r] = __popcll(m);
-    }
-}
-__device__ __forceinline__ void end(int r) {
-    if (leader()) {
-        const unsigned long long dt = now() - t0[threadIdx.x >> 6][r];
-        acc[threadIdx.x >> 6][r] += dt;
-        accl[threadIdx.x >> 6][r] += dt * n0[threadIdx.x >> 6][r];
-    }
-}
-__device__ __forceinline__ void prof(int k) {
-    const unsigned long long m = __ballot(1);
-    if (leader()) {
-        pw[threadIdx.x >> 6][k] += 1;
-        pl[threadIdx.x >> 6][k] += __popcll(m);
-    }
-}
-__device__ __forceinline__ void poly_begin() { begin(R_POLY); }
-__device__ __forceinline__ void poly_end() { end(R_POLY); }
-__device__ __forceinline__ void prefix_begin() { begin(R_PREFIX); }
-__device__ __forceinline__ void prefix_end() { end(R_PREFIX); }
-__device__ __forceinline__ void halve_begin() { begin(R_HALVE); }
-__device__ __forceinline__ void halve_end() { end(R_HALVE); }
-__device__ __forceinline__ void adv_begin() { begin(R_ADV); }
-__device__ __forceinline__ void adv_end() { end(R_ADV); }
-__device__ __forceinline__ void lit_begin() { begin(R_LIT); }
-}  // namespace mreg
-}  // namespace pt
-#define PT_MREG(what) pt::mreg::what()
-#define PT_MPROF(field) (pt::mreg::prof(pt::mreg::P_##field))
-#endif
+#include "pt_lprof.hpp"  // tuning instrumentation (compiled out of the product builds)
 
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
@@ -312,27 +253,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
     PT_LP_BEGIN();
-#ifdef PT_BOUNCE_LANES
-    // Tuning builds only (with the diag build): wave cycles between
-    // consecutive stamps, charged to the section the stamp ends and weighted
-    // by the lanes active at it, by the wave's first active lane (no forced
-    // waits): where the bounce's lanes idle.
-    __shared__ unsigned long long bl_t0[4], bl_acc[4][7], bl_lan[4][7];
-    if (DIAG && (threadIdx.x & 63) == 0) {
-        bl_t0[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
-        for (int k = 0; k < 7; k++) bl_acc[threadIdx.x >> 6][k] = bl_lan[threadIdx.x >> 6][k] = 0;
-    }
-#define PT_BSTAMP(k)                                                                              \
-    if (DIAG) {                                                                                   \
-        const unsigned long long m_ = __ballot(1);                                               \
-        if (lane_id() == (uint32_t)__builtin_ctzll(m_)) {                                        \
-            const unsigned long long n_ = __builtin_amdgcn_s_memtime(), d_ = n_ - bl_t0[threadIdx.x >> 6]; \
-            bl_acc[threadIdx.x >> 6][k] += d_;                                                   \
-            bl_lan[threadIdx.x >> 6][k] += d_ * __popcll(m_);                                    \
-            bl_t0[threadIdx.x >> 6] = n_;                                                        \
-        }                                                                                         \
-    }
-#else
 #define PT_BSTAMP(k)                                                \
     if (DIAG) {                                                     \
         __builtin_amdgcn_s_waitcnt(0);                              \
@@ -340,7 +260,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         dsec[k] += n_ - tst;                                        \
         tst = n_;                                                   \
     }
-#endif
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         if (DIAG) tst = __builtin_amdgcn_s_memtime();
         const uint32_t i = base + threadIdx.x;
@@ -480,16 +399,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
     }
 #undef PT_BSTAMP
     PT_LP_END();
-#ifdef PT_BOUNCE_LANES
-    if (DIAG && (threadIdx.x & 63) == 0)
-        for (int k = 0; k < 7; k++) {
-            atomicAdd(&diag[36 + k], bl_acc[threadIdx.x >> 6][k]);
-            atomicAdd(&diag[48 + k], bl_lan[threadIdx.x >> 6][k]);
-        }
-#else
     if (DIAG && (threadIdx.x & 63) == 0)
         for (int k = 0; k < 7; k++) atomicAdd(&diag[36 + k], dsec[k]);
-#endif
 }
 
 // Fused bounces (PT_WF_FUSED=1; measured slower, see fused_bounces()): a lane carries its path through as
@@ -898,9 +809,6 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     bool marching = false;
     int km = 0, mshape = -1;
     auto start_job = [&](uint32_t k) {  // k: queue position
-#ifdef PT_TIMING_CONVERGED  // timing experiment only: every lane of an aligned run of 64 takes the run's first job
-        k = (k / 64) * 64;
-#endif
         const uint32_t id = mq[k];  // position in the bounce's output
         if (pre) {
             cur.id = id;
@@ -915,14 +823,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
             load_job(v.out, id, &cur);
         }
     };
-#ifdef PT_MARCH_REGIONS
-    if ((threadIdx.x & 63) == 0) {
-        for (int k = 0; k < mreg::R_N; k++)
-            mreg::t0[threadIdx.x >> 6][k] = mreg::acc[threadIdx.x >> 6][k] = mreg::accl[threadIdx.x >> 6][k] = 0;
-        for (int k = 0; k < mreg::P_N; k++) mreg::pw[threadIdx.x >> 6][k] = mreg::pl[threadIdx.x >> 6][k] = 0;
-    }
-    const unsigned long long t_kernel = mreg::now();
-#endif
+    PT_MREG_KERNEL_BEGIN();
     if (have) start_job(pos(q));
     V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
@@ -956,19 +857,9 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         {
             bool done = false;
             if (marching) {
-#ifdef PT_MARCH_REGIONS
-                mreg::begin(mreg::R_ITER);
+                PT_MREG_STEP_BEGIN();
                 const int st = march::march_step<false, true, FK>(ms, &mst);
-                mreg::end(mreg::R_ITER);
-                if (mreg::leader() && mreg::t0[threadIdx.x >> 6][mreg::R_LIT]) {  // a literal loop ran: close it
-                    const unsigned long long dt = mreg::now() - mreg::t0[threadIdx.x >> 6][mreg::R_LIT];
-                    mreg::acc[threadIdx.x >> 6][mreg::R_LIT] += dt;
-                    mreg::accl[threadIdx.x >> 6][mreg::R_LIT] += dt * mreg::n0[threadIdx.x >> 6][mreg::R_LIT];
-                    mreg::t0[threadIdx.x >> 6][mreg::R_LIT] = 0;
-                }
-#else
-                const int st = march::march_step<false, true, FK>(ms, &mst);
-#endif
+                PT_MREG_STEP_END();
                 if (st != march::M_RUNNING) {
                     if (st == march::M_GUARD) dev::note_guard(sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
@@ -998,9 +889,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 done = !marching;
             }
             if (done) {
-#ifdef PT_MARCH_REGIONS
-                mreg::begin(mreg::R_REFILL);
-#endif
+                PT_MREG_REFILL_BEGIN();
                 // vmcnt counts loads and stores in issue order: a store issued
                 // before the next job's loads makes the wait for those loads a
                 // wait for the store's completion too, so the finished job's
@@ -1017,27 +906,11 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
                 }
-#ifdef PT_MARCH_REGIONS
-                mreg::end(mreg::R_REFILL);
-#endif
+                PT_MREG_REFILL_END();
             }
         }
     }
-#ifdef PT_MARCH_REGIONS
-    if ((threadIdx.x & 63) == 0) {
-        const int w = threadIdx.x >> 6;
-        mreg::acc[w][mreg::R_TOTAL] = mreg::now() - t_kernel;
-        mreg::accl[w][mreg::R_TOTAL] = 0;
-        for (int k = 0; k < mreg::R_N; k++) {
-            atomicAdd(&mreg::g_acc[k], mreg::acc[w][k]);
-            atomicAdd(&mreg::g_acc[mreg::R_N + k], mreg::accl[w][k]);
-        }
-        for (int k = 0; k < mreg::P_N; k++) {
-            atomicAdd(&mreg::g_acc[2 * mreg::R_N + k], mreg::pw[w][k]);
-            atomicAdd(&mreg::g_acc[2 * mreg::R_N + mreg::P_N + k], mreg::pl[w][k]);
-        }
-    }
-#endif
+    PT_MREG_KERNEL_END();
     if (DIAG && (threadIdx.x & 63) == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         if (mask_prev >= 0) {
@@ -1514,9 +1387,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (sc.nmarch == 0) continue;  // no ray-marched shape: the march queue is always empty
-#ifdef PT_ABL_NOMARCH
-                continue;  // timing ablation only (not exact): the march kernel's share of the frame
-#endif
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)

@@ -6,7 +6,7 @@
 #   bash scripts/gpu.sh tests    <tag> [pytest -k expr]   GPU test suite
 #   bash scripts/gpu.sh smoke    <tag>                    __graft_entry__.smoke()
 #   bash scripts/gpu.sh bench    <tag> [bench args...]    one bench.py line -> <tag>/bench.log
-#   bench A/B of tuning knobs:   PT_WF_SLOTS=1 bash scripts/gpu.sh bench <tag> --no-cpu-baseline
+#   bench A/B of tuning knobs:   bash scripts/gpu.sh bench <tag> --no-cpu-baseline --option wf_slots=1
 #   bash scripts/gpu.sh kt       <tag> [bench args...]    rocprofv3 --kernel-trace --stats of bench.py
 #   bash scripts/gpu.sh pmc      <tag> [bench args...]    FETCH_SIZE / WRITE_SIZE passes (separate runs)
 #                                                         -> <tag>/pmc_traffic.json (scripts/pmc_traffic.py)

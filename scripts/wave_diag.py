@@ -19,8 +19,8 @@ d = pt.wave_diag(r, False)
 trips, cyc, lanes = d[:16], d[16:32], d[32:36]
 bsec = d[36:43]
 blan = d[48:55]
-print("bounce sections (wave cycles; a PT_BOUNCE_LANES build: lanes active at each section's end, no forced "
-      "waits; otherwise each section ended by a full wait): " + ", ".join(
+print("bounce sections (wave cycles of the diag build, each section ended by a full wait; lanes: "
+      "scripts/bounce_lanes.py): " + ", ".join(
     "%s %.1f%%%s" % (n, 100 * x / max(1, sum(bsec)), (" (%.1f lanes)" % (l / x)) if any(blan) and x else "")
     for n, x, l in zip(["list", "state", "shade", "end", "trace", "precheck", "store"], bsec, blan)))
 names = ["cheap", "select", "adv", "proof"]

@@ -47,7 +47,7 @@ def test_c3_full_size_frame(pt, cornell):
 
 
 def test_c3_chunked_equals_unchunked(pt, cornell):
-    """The full-size frame cut into 1-spp chunks and tile groups (PT_WF_PATHS)
+    """The full-size frame cut into 1-spp chunks and tile groups (the wf_paths option)
     sums the same samples in the same order as one chunk."""
     ps, _ = cornell
     cam = ps.camera()

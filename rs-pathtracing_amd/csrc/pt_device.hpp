@@ -96,7 +96,7 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 #define PT_SLAB32 0  // A/B knob: the large-tree builds' BVH slab test in f32 with a conservative widening
 #endif
 #ifndef PT_AXIS_LEAF
-#define PT_AXIS_LEAF 0  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t (A/B knob)
+#define PT_AXIS_LEAF 1  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t (C5 +3.3 %, round-4 A/B r4b)
 #endif
 
 // ------------------------------------------------------------ primitives

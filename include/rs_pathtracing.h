@@ -30,6 +30,7 @@ extern "C" {
 #define PT_ERR_UNSUPPORTED -3 /* valid reference JSON the GPU path does not take  */
 #define PT_ERR_HIP -4         /* HIP runtime failure                               */
 #define PT_ERR_STATE -5       /* call out of order (e.g. step before start)       */
+#define PT_ERR_IO -6          /* unreadable / corrupt file (pt_checkpoint_load)   */
 
 /* shape kinds */
 #define PT_SPHERE 0    /* src/world/shapes/mod.rs:304-399 */
@@ -226,6 +227,49 @@ uint32_t pt_shard_tiles(uint32_t width, uint32_t height, uint32_t rank, uint32_t
 int pt_unshard_device(int device, const double *d_gathered, uint32_t width, uint32_t height, uint32_t world,
                       double *d_frame, void *hip_stream);
 
+/* ---- resumable frames (checkpoint / resume) ----------------------------- */
+/* The reference renders a frame in one go and keeps nothing between runs
+ * (Renderer::render, src/renderer/mod.rs:67-114; its GUI saves only the
+ * encoded image, src/bin/main.rs:281-289).  A frame here can be cut into
+ * sample windows instead: pt_render_device_samples renders samples
+ * [s_begin, s_end) of exactly the frame pt_render_device(..., samples_number,
+ * ...) renders, into the same d_out layout.  d_out holds per-pixel running
+ * sums between windows: read when s_begin > 0 (the sums of samples
+ * [0, s_begin)), written as sums when s_end < samples_number and as the
+ * means when s_end == samples_number.  Each sample keeps its frame-wide
+ * index (its RNG key, pt_sample_key) and the sums add samples in index
+ * order, so windows [0, a), [a, b), ..., [z, spp) leave d_out bit-identical to
+ * one pt_render_device call.  0 <= s_begin < s_end <= samples_number, else
+ * PT_ERR_INVALID.  Always runs the wavefront engine. */
+int pt_render_device_samples(pt_renderer *r, const pt_camera *camera, uint32_t width, uint32_t height,
+                             uint32_t samples_number, uint64_t seed, uint32_t rank, uint32_t world,
+                             uint32_t s_begin, uint32_t s_end, double *d_out, void *hip_stream);
+/* A checkpoint file: the 8 bytes "PTCKPT01", this header, `count` doubles
+ * (the running sums of one rank's d_out after samples [0, samples_done)) and
+ * a 64-bit FNV-1a checksum over the preceding bytes taken as little-endian
+ * 64-bit words; all little-endian.  scene_key is the caller's: any value
+ * that names the scene, camera and renderer options the sums belong to (the
+ * Python mirror hashes the scene JSON, the camera and the depth); a resumed
+ * frame must present the same key (checked by the caller). */
+typedef struct pt_checkpoint {
+    uint32_t width, height, samples_number, samples_done;
+    uint32_t rank, world, depth, reserved; /* reserved: 0 */
+    uint64_t seed;
+    uint64_t scene_key;
+    uint64_t count; /* doubles of sums: width*height*3 (world 1) or pt_shard_tiles(...)*768 */
+} pt_checkpoint;
+/* Writes header + sums[0..count) to path (atomically: a temporary file renamed
+ * over it).  The header must be consistent (samples_done <= samples_number,
+ * rank < world, count as above), else PT_ERR_INVALID. */
+int pt_checkpoint_save(const char *path, const pt_checkpoint *c, const double *sums);
+/* Reads path's header into *c and, when sums is not NULL, its count sums
+ * (capacity: doubles available at sums; fewer than count -> PT_ERR_INVALID)
+ * and checks the checksum (a header-only read checks format, header and file
+ * size).  A file that is missing, short, long, of another format, with an
+ * inconsistent header or a checksum mismatch -> PT_ERR_IO with a message;
+ * sums is zeroed on a checksum mismatch. */
+int pt_checkpoint_load(const char *path, pt_checkpoint *c, double *sums, uint64_t capacity);
+
 /* ---- probes on the GPU (reference pub fns) ----------------------------- */
 /* Scene::closest_hit (src/world/mod.rs:42-44) for n rays (origin, direction:
  * 6 doubles each).  out[i].shape = -1 on a miss. */
@@ -334,6 +378,7 @@ uint32_t pt_abi_version(void);
 #define PT_ABI_SHAPE_INFO 2    /* 20 fields, as declared */
 #define PT_ABI_MATERIAL_INFO 3 /* 6 fields */
 #define PT_ABI_HIT 4           /* 7 fields */
+#define PT_ABI_CHECKPOINT 5    /* 11 fields, as declared */
 int pt_abi_layout(int which, uint32_t *out, size_t n);
 
 #ifdef __cplusplus

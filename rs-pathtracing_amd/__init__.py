@@ -20,7 +20,9 @@ from __future__ import annotations
 
 import abc
 import ctypes as C
+import hashlib
 import os
+import struct
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -30,7 +32,7 @@ PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "librs_pathtracing_amd.so"
 
 PT_OK = 0
-PT_ERR_INVALID, PT_ERR_PARSE, PT_ERR_UNSUPPORTED, PT_ERR_HIP, PT_ERR_STATE = -1, -2, -3, -4, -5
+PT_ERR_INVALID, PT_ERR_PARSE, PT_ERR_UNSUPPORTED, PT_ERR_HIP, PT_ERR_STATE, PT_ERR_IO = -1, -2, -3, -4, -5, -6
 SPHERE, RECTANGLE, CUBE, MARCH, TORUS = 0, 1, 2, 3, 4
 LAMBERTIAN, METAL, DIELECTRIC, DIFFUSE_LIGHT, EMPTY = 0, 1, 2, 3, 4
 TILE = 16
@@ -46,6 +48,7 @@ EXPORTS = [
     "pt_ray_color", "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_march_guard_drops", "pt_wave_diag",
     "pt_kernel_timing", "pt_encode_rgba8", "pt_encode_rgba8_device", "pt_write_png", "pt_write_ppm",
     "pt_sample_key", "pt_last_error", "pt_version", "pt_abi_version", "pt_abi_layout", "pt_renderer_peer_access",
+    "pt_render_device_samples", "pt_checkpoint_save", "pt_checkpoint_load",
 ]
 ABI_VERSION = 3  # PT_ABI_VERSION this binding is written for
 
@@ -91,6 +94,12 @@ class HitStruct(C.Structure):
     _fields_ = [("t", C.c_double), ("point", C.c_double * 3), ("normal", C.c_double * 3),
                 ("front_face", C.c_int32), ("shape", C.c_int32), ("material", C.c_int32),
                 ("pad0", C.c_int32)]
+
+
+class CheckpointStruct(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("samples_number", C.c_uint32),
+                ("samples_done", C.c_uint32), ("rank", C.c_uint32), ("world", C.c_uint32), ("depth", C.c_uint32),
+                ("reserved", C.c_uint32), ("seed", C.c_uint64), ("scene_key", C.c_uint64), ("count", C.c_uint64)]
 
 
 HIT_DTYPE = np.dtype([("t", "<f8"), ("point", "<f8", 3), ("normal", "<f8", 3), ("front_face", "<i4"),
@@ -142,6 +151,10 @@ def lib():
         "pt_render_stop": (C.c_int, [vp]),
         "pt_render_device": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, u32, u32, vp, vp]),
         "pt_render_frame_device": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, vp, vp]),
+        "pt_render_device_samples": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, u32, u32, u32, u32,
+                                               vp, vp]),
+        "pt_checkpoint_save": (C.c_int, [C.c_char_p, C.POINTER(CheckpointStruct), d]),
+        "pt_checkpoint_load": (C.c_int, [C.c_char_p, C.POINTER(CheckpointStruct), d, u64]),
         "pt_shard_tiles": (u32, [u32, u32, u32, u32]),
         "pt_unshard_device": (C.c_int, [C.c_int, vp, u32, u32, u32, vp, vp]),
         "pt_closest_hit": (C.c_int, [vp, d, sz, C.c_double, C.c_double, vp]),
@@ -393,6 +406,14 @@ class HipRenderer(Renderer):
         _check(lib().pt_render_device(self._h, C.byref(camera._c), width, height, spp, seed, rank, world,
                                       C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
 
+    def render_device_samples(self, camera: Camera, width: int, height: int, spp: int, seed: int, rank: int,
+                              world: int, s_begin: int, s_end: int, out_ptr: int, stream_ptr: int = 0):
+        """Samples [s_begin, s_end) of the frame render_device renders, added to the running sums at out_ptr
+        (read when s_begin > 0; sums stored, or the means once s_end == spp; see pt_render_device_samples)."""
+        _check(lib().pt_render_device_samples(self._h, C.byref(camera._c), width, height, spp, seed, rank, world,
+                                              int(s_begin), int(s_end), C.c_void_p(out_ptr),
+                                              C.c_void_p(stream_ptr)))
+
     def render_frame_device(self, camera: Camera, width: int, height: int, spp: int, seed: int, frame_ptr: int,
                             stream_ptr: int = 0):
         """The whole frame over all of the renderer's devices into device memory at frame_ptr (first
@@ -586,6 +607,42 @@ def write_ppm(path, rgba: np.ndarray, width: int, height: int):
     _check(lib().pt_write_ppm(str(path).encode(), p, width, height))
 
 
+# ---- resumable frames -------------------------------------------------------
+def frame_key(scene_json: bytes, camera: Camera, depth: int, random_spheres: int = 1, scene_seed: int = 1) -> int:
+    """A 64-bit name for what a checkpoint's sums belong to: the scene text, the scene options, the camera
+    and the depth (pt_checkpoint.scene_key)."""
+    h = hashlib.blake2b(digest_size=8)
+    h.update(bytes(scene_json))
+    h.update(struct.pack("<IQI", int(random_spheres), int(scene_seed), int(depth)))
+    h.update(bytes(camera._c))
+    return int.from_bytes(h.digest(), "little")
+
+
+def checkpoint_count(width: int, height: int, rank: int = 0, world: int = 1) -> int:
+    """Doubles in a rank's running sums (pt_render_device's d_out layout)."""
+    return width * height * 3 if world == 1 else shard_tiles(width, height, rank, world) * TILE * TILE * 3
+
+
+def save_checkpoint(path, sums: np.ndarray, *, width: int, height: int, samples_number: int, samples_done: int,
+                    seed: int, depth: int, scene_key: int = 0, rank: int = 0, world: int = 1):
+    """Write a rank's running sums after samples [0, samples_done) (pt_checkpoint_save)."""
+    sums = np.ascontiguousarray(sums, dtype=np.float64).reshape(-1)
+    c = CheckpointStruct(width, height, samples_number, samples_done, rank, world, depth, 0, seed, scene_key,
+                         sums.size)
+    _check(lib().pt_checkpoint_save(str(path).encode(), C.byref(c), _dptr(sums)))
+
+
+def load_checkpoint(path, with_sums: bool = True):
+    """(header as a dict, sums as a float64 array or None) of a checkpoint file (pt_checkpoint_load)."""
+    c = CheckpointStruct()
+    _check(lib().pt_checkpoint_load(str(path).encode(), C.byref(c), None, 0))
+    sums = None
+    if with_sums:
+        sums = np.empty(c.count, dtype=np.float64)
+        _check(lib().pt_checkpoint_load(str(path).encode(), C.byref(c), _dptr(sums), sums.size))
+    return {k: getattr(c, k) for k, _ in CheckpointStruct._fields_}, sums
+
+
 def sample_key(seed: int, pixel: int, sample: int) -> int:
     return lib().pt_sample_key(seed, pixel, sample)
 
@@ -601,7 +658,7 @@ def source_id() -> str:
 
 
 # pt_abi_layout struct ids and the ctypes mirror of each
-ABI_STRUCTS = {0: SceneOpts, 1: CameraStruct, 2: ShapeInfo, 3: MaterialInfo, 4: HitStruct}
+ABI_STRUCTS = {0: SceneOpts, 1: CameraStruct, 2: ShapeInfo, 3: MaterialInfo, 4: HitStruct, 5: CheckpointStruct}
 
 
 def abi_layout(which: int) -> list:

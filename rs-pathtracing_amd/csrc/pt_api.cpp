@@ -166,6 +166,13 @@ int pt_abi_layout(int which, uint32_t *out, size_t n) {
         PT_F(pt_hit, t), PT_F(pt_hit, point), PT_F(pt_hit, normal), PT_F(pt_hit, front_face);
         PT_F(pt_hit, shape), PT_F(pt_hit, material), PT_F(pt_hit, pad0);
         break;
+    case PT_ABI_CHECKPOINT:
+        v.push_back(sizeof(pt_checkpoint));
+        PT_F(pt_checkpoint, width), PT_F(pt_checkpoint, height), PT_F(pt_checkpoint, samples_number);
+        PT_F(pt_checkpoint, samples_done), PT_F(pt_checkpoint, rank), PT_F(pt_checkpoint, world);
+        PT_F(pt_checkpoint, depth), PT_F(pt_checkpoint, reserved), PT_F(pt_checkpoint, seed);
+        PT_F(pt_checkpoint, scene_key), PT_F(pt_checkpoint, count);
+        break;
     default:
         return fail(PT_ERR_INVALID, "pt_abi_layout: unknown struct " + std::to_string(which));
     }
@@ -878,9 +885,17 @@ uint32_t pt_shard_tiles(uint32_t w, uint32_t h, uint32_t rank, uint32_t world) {
 
 int pt_render_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp, uint64_t seed,
                      uint32_t rank, uint32_t world, double *d_out, void *stream) {
+    return pt_render_device_samples(r, cam, w, h, spp, seed, rank, world, 0, spp, d_out, stream);
+}
+
+int pt_render_device_samples(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h, uint32_t spp,
+                             uint64_t seed, uint32_t rank, uint32_t world, uint32_t s_begin, uint32_t s_end,
+                             double *d_out, void *stream) {
     if (!r || !cam || !d_out) return fail(PT_ERR_INVALID, "null argument");
     if (w == 0 || h == 0 || spp == 0) return fail(PT_ERR_INVALID, "width, height and samples_number must be > 0");
     if (world == 0 || rank >= world) return fail(PT_ERR_INVALID, "rank must be < world");
+    if (s_begin >= s_end || s_end > spp)
+        return fail(PT_ERR_INVALID, "sample window must satisfy 0 <= s_begin < s_end <= samples_number");
     if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
     GpuShare &g = r->gpus[0];
     HIP_TRY(hipSetDevice(g.device));
@@ -890,6 +905,8 @@ int pt_render_device(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t 
     P.compact = world > 1 ? 1 : 0;
     P.tile_begin = 0;
     P.tile_count = pt_shard_tiles(w, h, rank, world);
+    P.s_begin = s_begin;
+    P.s_end = s_end;
     // any HIP stream of the renderer's (first) device, 0 being the null stream
     // as everywhere in HIP (pt_unshard_device takes the same handle, so a
     // caller's render -> gather -> unshard stays ordered)

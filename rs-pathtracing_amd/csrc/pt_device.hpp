@@ -93,10 +93,12 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 }
 
 #ifndef PT_SLAB32
-#define PT_SLAB32 0  // A/B knob: the large-tree builds' BVH slab test in f32 with a conservative widening
+#define PT_SLAB32 1  // the large-tree builds' BVH slab test in f32 with a conservative widening (C5 +1.3 %, r4f)
 #endif
 #ifndef PT_AXIS_LEAF
-#define PT_AXIS_LEAF 1  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t (C5 +3.3 %, round-4 A/B r4b)
+#define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,
+                        // 2 in the large-tree (FMA_SLAB) builds only (C5 +3.2 %; in the C2 bounce the extra path
+                        // costs 9 %: round-4 A/B r4g)
 #endif
 
 // ------------------------------------------------------------ primitives
@@ -442,18 +444,19 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     auto tx = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.x, mx) : ((double)b - r.o.x) * inv.x; };
     auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
     auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };
-    const bool axis_ok = PT_AXIS_LEAF && axis_ray_ok(r.o, r.d);
+    const bool axis_ok = (PT_AXIS_LEAF == 1 || (PT_AXIS_LEAF == 2 && FMA_SLAB)) && axis_ray_ok(r.o, r.d);
     // SLAB32 (PT_SLAB32, the FMA_SLAB builds): the planes' t in f32, t = fma(b, 1/d, -o/d), widened on each
     // axis by e = 2^-21 (B + |o|) |1/d| (B >= every plane's |b|): against the real t = (b - o) / d, the f32
     // 1/d and -o/d (each 2^-24 relative, after the f64 rounding), the fma's rounding and the widening's own
     // rounding add up to less than 1.6 * 2^-23 (|b| + |o|) |1/d|, so the widened interval contains the real
     // one and the cull stays conservative (1e-30 more covers an f32 flush of tiny values).  An axis whose
-    // 1/d or -o/d does not fit an f32 is left open (NaN t's drop out of fmax/fmin); min_t is rounded down and
-    // best up.  The hits are decided by the exact f64 leaf tests as in every walk.
+    // 1/d or -o/d does not fit an f32 is left open (NaN t's drop out of fmax/fmin), and so is one whose |1/d| is
+    // below 1e-30, where an f32 flush of b * 1/d could exceed the widening; min_t is rounded down and best up.
+    // The hits are decided by the exact f64 leaf tests as in every walk.
     constexpr bool S32 = FMA_SLAB && PT_SLAB32;
     auto axis32 = [&](double o, double iv, float *i32, float *m32, float *e32) {
         const double m = -(o * iv);
-        const bool fits = fabs(iv) < 1e30 && fabs(m) < 1e30;
+        const bool fits = fabs(iv) < 1e30 && fabs(iv) > 1e-30 && fabs(m) < 1e30;
         *i32 = (float)iv;
         *m32 = fits ? (float)m : __builtin_nanf("");
         *e32 = (float)((0x1p-21 * (1.0 + 0x1p-20)) * ((double)sc.bvh_bound + fabs(o)) * fabs(iv) + 1e-30);

@@ -363,6 +363,11 @@ static bool use_wavefront(const DeviceScene &s, const FrameParams &P, WaveWorksp
 hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out, hipStream_t st,
                          WaveWorkspace *ws) {
     if (P.tile_count == 0) return hipSuccess;
+    if (P.s_begin > 0 || (P.s_end && P.s_end < P.spp)) {
+        // a sample window: only the wavefront engine keeps running sums across launches
+        if (!ws || P.s_begin >= (P.s_end ? P.s_end : P.spp)) return hipErrorInvalidValue;
+        return launch_render_wave(dscene(s), P, out, st, ws, s.fkind);
+    }
     if (use_wavefront(s, P, ws)) return launch_render_wave(dscene(s), P, out, st, ws, s.fkind);
     KernelTimer *tm = ws ? ws->timer : nullptr;
     hipError_t e0 = timer_begin(tm, st, K_MEGA);

@@ -99,6 +99,11 @@ struct FrameParams {
     uint32_t width, height, spp, depth;
     uint32_t rank, world, tiles_x, tile_begin;
     uint32_t tile_count, compact;
+    // sample window [s_begin, s_end) of a resumable frame (pt_render_device_samples; s_end 0 = spp): the launch
+    // adds those samples to the per-pixel running sums in `out` (read when s_begin > 0) and stores the sums,
+    // or the means when s_end = spp; samples keep their frame-wide indices, so the windows' results are the
+    // whole frame's bit for bit
+    uint32_t s_begin, s_end;
     // progressive frames: the renderer's stop flag in host-mapped memory
     // (pt_render_stop sets it while it drains the queued launches); null: none
     const int *stop;

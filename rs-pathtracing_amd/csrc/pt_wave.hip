@@ -44,13 +44,6 @@
 #include "pt_device.hpp"
 #include "pt_kernel.hpp"
 
-#ifndef PT_LEAF_AOS
-#define PT_LEAF_AOS 0  // A/B knob: an ended path's leaf radiance and depth as one 32-byte record per slot
-#endif
-#ifndef PT_SOA_OPAQUE
-#define PT_SOA_OPAQUE 0  // A/B knob: path-state addresses formed per iteration (scalar) instead of spilled
-#endif
-
 namespace pt {
 
 using dev::Ray;
@@ -84,10 +77,11 @@ struct PathSoA {
 // Device view of the workspace for one chunk.
 struct WfView {
     PathSoA in, out;  // the bounce reads `in` (by list position) and writes `out` (by its input index)
-    uint32_t *fin;   // per slot: attenuation-stack depth when the path ended (wf_reduce unwinds it)
     uint32_t *ids;   // attenuation-id stack: entry k of a path at ids[k * cap + id]
     double *att;     // textured attenuation values (EXT builds): (k * 3 + c) * cap + id
-    double *rx, *ry, *rz;  // sample radiance of finished paths
+    // per slot, 32 B: an ended path's leaf radiance (x, y, z) and its attenuation-stack depth (u64 bits; wf_reduce
+    // unwinds the stack)
+    double *leaf;
     uint8_t *status;  // per output position of a bounce: bit 0 path alive, bit 1 needs a march, bit 2 long march
     uint32_t *list, *mq;  // positions (in `out` of the previous / current bounce) of the live paths and march jobs
     // march jobs pre-selected by the bounce kernel (scenes with one ray-marched
@@ -172,20 +166,14 @@ __device__ __forceinline__ V3 unwind_mem(const dev::Scene &sc, MemStack &stk, V3
 // (the recursion's products, in its order) when it sums the chunk's samples,
 // so the bounce kernel's waves never wait for the unwind's dependent loads.
 // Non-temporal (read once, by the chunk's reduce): iso bounce -0.6 ms, C2 +0.4 %.
-// (PT_LEAF_AOS) the leaf and the depth as one 32-byte record per slot at v.rx (two 16-byte stores): an ended
-// path's write touches one line instead of four (rx, ry, rz, fin), and only ~1 lane in 8 ends per bounce.
+// The leaf and the depth form one 32-byte record per slot (two 16-byte stores): an ended path's write touches
+// one line instead of the four of separate x / y / z / depth arrays, where only ~1 lane in 8 ends per bounce
+// (C2 iso bounce 226.4 -> 222.0 ms, +1.1..2.8 %, round-4 A/B r4f).
 __device__ __forceinline__ void end_path(const WfView &v, uint32_t id, const MemStack &stk, V3 leaf) {
-    if (PT_LEAF_AOS) {
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        d2v *rec = (d2v *)(v.rx + (size_t)id * 4);
-        __builtin_nontemporal_store((d2v){leaf.x, leaf.y}, rec);
-        __builtin_nontemporal_store((d2v){leaf.z, __builtin_bit_cast(double, (uint64_t)(uint32_t)stk.n)}, rec + 1);
-        return;
-    }
-    __builtin_nontemporal_store(leaf.x, v.rx + id);
-    __builtin_nontemporal_store(leaf.y, v.ry + id);
-    __builtin_nontemporal_store(leaf.z, v.rz + id);
-    __builtin_nontemporal_store((uint32_t)stk.n, v.fin + id);
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    d2v *rec = (d2v *)(v.leaf + (size_t)id * 4);
+    __builtin_nontemporal_store((d2v){leaf.x, leaf.y}, rec);
+    __builtin_nontemporal_store((d2v){leaf.z, __builtin_bit_cast(double, (uint64_t)(uint32_t)stk.n)}, rec + 1);
 }
 
 // A live path's state at output position k: non-temporal stores (the state
@@ -290,9 +278,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
                 PathSoA S = v.in;
-                // (PT_SOA_OPAQUE) the set's size made opaque here, so its 11 array addresses are formed per
-                // iteration with scalar ops rather than held across the loop in spilled SGPRs (v_readlane)
-                if (PT_SOA_OPAQUE) asm volatile("" : "+s"(S.cap));
                 id = ld_path(S.sid() + p);
                 ray.o = dev::v3(ld_path(S.ox() + p), ld_path(S.oy() + p), ld_path(S.oz() + p));
                 ray.d = dev::v3(ld_path(S.dx() + p), ld_path(S.dy() + p), ld_path(S.dz() + p));
@@ -390,9 +375,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         if (i < count) PT_LP(STORE);
         if (i < count)
         {
-            PathSoA O = v.out;
-            if (PT_SOA_OPAQUE) asm volatile("" : "+s"(O.cap));
-            store_path(O, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+            store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
         }
         if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         PT_BSTAMP(6)
@@ -925,7 +908,8 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     }
 }
 
-// In-order per-pixel sum of the chunk's samples; mean after the last chunk.
+// In-order per-pixel sum of the chunk's samples; mean after the last chunk (a
+// sample window's running sums instead when it ends short of spp).
 // Each sample's radiance is first unwound from its path's end: the leaf
 // radiance times the attenuations its stack holds, in the recursion's order
 // (dev::unwind; end_path left the leaf and the stack depth).  Sample by
@@ -947,21 +931,18 @@ __global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, W
         if (P.compact && last) dst[0] = dst[1] = dst[2] = 0.0;
         return;
     }
-    V3 a = first ? dev::v3(0.0, 0.0, 0.0) : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
+    V3 a = first == 1   ? dev::v3(0.0, 0.0, 0.0)
+           : first == 2 ? dev::v3(dst[0], dst[1], dst[2])
+                        : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
     for (uint32_t s = 0; s < v.ns; s++) {
         const size_t id = (size_t)s * v.npix + pl;
-        if (PT_LEAF_AOS) {
-            const double *rec = v.rx + id * 4;
-            const uint32_t fin = (uint32_t)__builtin_bit_cast(uint64_t, rec[3]);
-            MemStack stk{v.ids + id, (size_t)v.cap, (int)fin, EXT ? v.att + id : nullptr};
-            a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(rec[0], rec[1], rec[2])));
-        } else {
-            MemStack stk{v.ids + id, (size_t)v.cap, (int)v.fin[id], EXT ? v.att + id : nullptr};
-            a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(v.rx[id], v.ry[id], v.rz[id])));
-        }
+        const double *rec = v.leaf + id * 4;
+        const uint32_t fin = (uint32_t)__builtin_bit_cast(uint64_t, rec[3]);
+        MemStack stk{v.ids + id, (size_t)v.cap, (int)fin, EXT ? v.att + id : nullptr};
+        a = dev::add(a, unwind_mem<EXT>(sc, stk, dev::v3(rec[0], rec[1], rec[2])));
     }
     if (last) {
-        const V3 c = dev::divs(a, (double)P.spp);
+        const V3 c = last == 2 ? a : dev::divs(a, (double)P.spp);
         dst[0] = c.x;
         dst[1] = c.y;
         dst[2] = c.z;
@@ -1194,6 +1175,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                                  WaveWorkspace *ws, int fkind) {
     const Tuning &tu = ws->tune;
     const uint32_t cap_want = (uint32_t)tu.wf_paths;
+    // the launch's samples: the frame's, or a resumable frame's window [s_begin, s_end) of them
+    const uint32_t s_begin = P0.s_begin, s_end = P0.s_end ? P0.s_end : P0.spp, nsw = s_end - s_begin;
     // tile groups (only for frames beyond cap_want pixels), then sample chunks
     const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
     const uint32_t ntiles = P0.tile_count;
@@ -1201,7 +1184,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const uint32_t npix_max = group_tiles * TILE * TILE;
     uint32_t ns = cap_want / npix_max;
     if (ns < 1) ns = 1;
-    if (ns > P0.spp) ns = P0.spp;
+    if (ns > nsw) ns = nsw;
     {
         // A small frame (one rank's share of a multi-GPU frame) still gets at
         // least wf_min_chunks sample chunks, so the pipelined slots overlap one
@@ -1209,7 +1192,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         // keep at least MIN_CHUNK_PATHS paths to fill the device.
         const uint32_t mc = (uint32_t)tu.wf_min_chunks;
         if (mc > 1 && ntiles <= group_tiles) {
-            uint32_t want = (P0.spp + mc - 1) / mc;
+            uint32_t want = (nsw + mc - 1) / mc;
             const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;
             if (want < floor_ns) want = floor_ns;
             if (want < ns) ns = want;
@@ -1220,7 +1203,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     const size_t cnt_words = (size_t)(iters + 2) * 4;
     const uint32_t cap_tiles = (cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
     // no more slots than chunks
-    const uint64_t chunks = (uint64_t)((ntiles + group_tiles - 1) / group_tiles) * ((P0.spp + ns - 1) / ns);
+    const uint64_t chunks = (uint64_t)((ntiles + group_tiles - 1) / group_tiles) * ((nsw + ns - 1) / ns);
     int slots = tu.wf_slots;
     if ((uint64_t)slots > chunks) slots = (int)chunks;
     hipError_t e = ensure_streams(ws, slots);
@@ -1234,9 +1217,9 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // pre-selected march jobs (one marched shape): the bounce kernel hands the march its object-space ray
     // and bound (C2 +9 %: iso march 340 -> 275 ms, bounce 248 -> 256, round 1)
     const bool presel = sc.nmarch == 1 && !ws->diag;
-    // two path-state sets (8 + 3 words per path each), sample radiances, lists, end depths
-    const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 8) * 3 +
-                              (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 3 +
+    // two path-state sets (8 + 3 words per path each), leaf records, lists
+    const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 32) +
+                              (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 2 +
                               al((size_t)cap * 4 * (P0.depth + 1)) +
                               al((size_t)cap_tiles * CP_TILE) + al(((size_t)cap_tiles + CP_BLOCK) * 12) + al(cnt_words * 4) +
                               al(att_bytes);
@@ -1258,16 +1241,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             S.base = (char *)take((size_t)cap * PathSoA::BYTES);
             S.cap = cap;
         }
-        v.fin = (uint32_t *)take((size_t)cap * 4);
         v.ids = (uint32_t *)take((size_t)cap * 4 * (P0.depth + 1));
-        if (PT_LEAF_AOS) {
-            v.rx = (double *)take((size_t)cap * 32);  // 32-byte leaf records (end_path)
-            v.ry = v.rz = nullptr;
-        } else {
-            v.rx = (double *)take((size_t)cap * 8);
-            v.ry = (double *)take((size_t)cap * 8);
-            v.rz = (double *)take((size_t)cap * 8);
-        }
+        v.leaf = (double *)take((size_t)cap * 32);  // 32-byte leaf records (end_path)
         v.list = (uint32_t *)take((size_t)cap * 4);
         v.mq = (uint32_t *)take((size_t)cap * 4);
         v.status = (uint8_t *)take((size_t)cap_tiles * CP_TILE);
@@ -1313,14 +1288,14 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // to whole rounds of `slots` (no round with an idle stream), with the
     // samples spread evenly over them (no short last chunk).  The per-pixel
     // sums take the chunks in sample order either way.
-    uint32_t nchunks = (P0.spp + ns - 1) / ns;
+    uint32_t nchunks = (nsw + ns - 1) / ns;
     if (slots > 1 && nchunks > 1 && nchunks % (uint32_t)slots) nchunks += (uint32_t)slots - nchunks % (uint32_t)slots;
-    if (nchunks > P0.spp) nchunks = P0.spp;
+    if (nchunks > nsw) nchunks = nsw;
     std::vector<Chunk> chunk_list;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        for (uint32_t c = 0, s0 = 0; c < nchunks; c++) {
-            const uint32_t n = P0.spp / nchunks + (c < P0.spp % nchunks ? 1u : 0u);  // <= ns
+        for (uint32_t c = 0, s0 = s_begin; c < nchunks; c++) {
+            const uint32_t n = nsw / nchunks + (c < nsw % nchunks ? 1u : 0u);  // <= ns
             chunk_list.push_back(Chunk{g0, gt, s0, n});
             s0 += n;
         }
@@ -1410,10 +1385,13 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             const uint32_t s0 = v.s0;
             if (slots > 1 && r0 + j > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
+            // first: 1 = sums from zero, 2 = from out's running sums; last: 1 = means, 2 = running sums to out
+            const int first = s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
+            const int last = s0 + v.ns >= s_end ? (s_end == P0.spp ? 1 : 2) : 0;
             if (sc.ext)
-                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, first, last, out);
             else
-                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, s0 == 0, s0 + v.ns >= P0.spp, out);
+                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, first, last, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;

@@ -88,12 +88,18 @@ static int do_layout(void) {
                            OFF(pt_material_info, emit)};
     const uint32_t hi[] = {sizeof(pt_hit), OFF(pt_hit, t), OFF(pt_hit, point), OFF(pt_hit, normal),
                            OFF(pt_hit, front_face), OFF(pt_hit, shape), OFF(pt_hit, material), OFF(pt_hit, pad0)};
+    const uint32_t ck[] = {sizeof(pt_checkpoint), OFF(pt_checkpoint, width), OFF(pt_checkpoint, height),
+                           OFF(pt_checkpoint, samples_number), OFF(pt_checkpoint, samples_done),
+                           OFF(pt_checkpoint, rank), OFF(pt_checkpoint, world), OFF(pt_checkpoint, depth),
+                           OFF(pt_checkpoint, reserved), OFF(pt_checkpoint, seed), OFF(pt_checkpoint, scene_key),
+                           OFF(pt_checkpoint, count)};
     int bad = 0;
     bad |= check("pt_scene_opts", PT_ABI_SCENE_OPTS, so, (int)(sizeof so / sizeof so[0]));
     bad |= check("pt_camera", PT_ABI_CAMERA, ca, (int)(sizeof ca / sizeof ca[0]));
     bad |= check("pt_shape_info", PT_ABI_SHAPE_INFO, sh, (int)(sizeof sh / sizeof sh[0]));
     bad |= check("pt_material_info", PT_ABI_MATERIAL_INFO, ma, (int)(sizeof ma / sizeof ma[0]));
     bad |= check("pt_hit", PT_ABI_HIT, hi, (int)(sizeof hi / sizeof hi[0]));
+    bad |= check("pt_checkpoint", PT_ABI_CHECKPOINT, ck, (int)(sizeof ck / sizeof ck[0]));
     if (pt_abi_layout(99, NULL, 0) != PT_ERR_INVALID) {
         fprintf(stderr, "unknown struct id accepted\n");
         bad = 1;
@@ -228,7 +234,45 @@ static int do_render(int argc, char **argv) {
     return 0;
 }
 
+/* A rank's running sums through a checkpoint file and back (host only). */
+static int do_checkpoint(const char *path) {
+    pt_checkpoint c;
+    memset(&c, 0, sizeof c);
+    c.width = 100;
+    c.height = 37;
+    c.samples_number = 64;
+    c.samples_done = 24;
+    c.rank = 1;
+    c.world = 2;
+    c.depth = 50;
+    c.seed = 7;
+    c.scene_key = 0x0123456789abcdefull;
+    c.count = (uint64_t)pt_shard_tiles(c.width, c.height, c.rank, c.world) * 256 * 3;
+    double *sums = malloc(c.count * sizeof(double)), *back = malloc(c.count * sizeof(double));
+    for (uint64_t i = 0; i < c.count; i++) sums[i] = (double)i * 0.1 - 3.0;
+    int rc = pt_checkpoint_save(path, &c, sums);
+    pt_checkpoint d;
+    if (rc == PT_OK) rc = pt_checkpoint_load(path, &d, back, c.count);
+    if (rc != PT_OK || memcmp(&c, &d, sizeof c) || memcmp(sums, back, c.count * sizeof(double))) {
+        fprintf(stderr, "round trip: status %d: %s\n", rc, pt_last_error());
+        return 1;
+    }
+    printf("checkpoint round trip: %llu sums\n", (unsigned long long)c.count);
+    FILE *f = fopen(path, "r+b");
+    if (!f || fseek(f, 8 + 56 + 8 * 1000 + 3, SEEK_SET) != 0 || fputc(0x5a, f) == EOF || fclose(f) != 0) return 1;
+    rc = pt_checkpoint_load(path, &d, back, c.count);
+    if (rc != PT_ERR_IO || back[1000] != 0.0) {
+        fprintf(stderr, "corrupt file: status %d\n", rc);
+        return 1;
+    }
+    printf("corrupt file refused: %s\n", pt_last_error());
+    free(sums);
+    free(back);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 3 && !strcmp(argv[1], "checkpoint")) return do_checkpoint(argv[2]);
     if (argc >= 2 && !strcmp(argv[1], "layout")) return do_layout();
     if (argc >= 3 && !strcmp(argv[1], "legacy")) return do_legacy(argv[2]);
     if (argc >= 2 && !strcmp(argv[1], "render")) return do_render(argc, argv);

@@ -93,7 +93,7 @@ def test_abi_version(pt):
     assert pt.lib().pt_abi_version() == pt.ABI_VERSION == 3
 
 
-@pytest.mark.parametrize("which", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4, 5])
 def test_abi_layout_matches_ctypes(pt, which):
     """pt_abi_layout (the library's own sizeof / offsetof) == the ctypes mirror."""
     S = pt.ABI_STRUCTS[which]
@@ -112,7 +112,7 @@ def test_plain_c_caller_layout():
     import subprocess
     out = subprocess.run([abi_check_bin(), "layout"], capture_output=True, text=True)
     assert out.returncode == 0, out.stderr
-    assert out.stdout.count("match") == 5
+    assert out.stdout.count("match") == 6
 
 
 def test_legacy_opts_keep_their_loader_and_are_not_read_past():
@@ -140,3 +140,12 @@ def test_opts_struct_size_from_python(pt, cornell_text):
         if rc == 0:
             assert L.pt_scene_num_shapes(h) == 9  # random_spheres = 0
             L.pt_scene_destroy(h)
+
+
+def test_plain_c_caller_checkpoint(tmp_path):
+    """The C caller writes a checkpoint of a 2-rank shard and reads it back
+    bit for bit; a flipped byte fails the checksum with PT_ERR_IO and zeroed sums."""
+    import subprocess
+    out = subprocess.run([abi_check_bin(), "checkpoint", str(tmp_path / "f.ckpt")], capture_output=True, text=True)
+    assert out.returncode == 0, (out.returncode, out.stderr)
+    assert "checkpoint round trip" in out.stdout and "corrupt file refused" in out.stdout

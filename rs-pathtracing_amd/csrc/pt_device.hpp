@@ -445,28 +445,34 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
     auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };
     const bool axis_ok = (PT_AXIS_LEAF == 1 || (PT_AXIS_LEAF == 2 && FMA_SLAB)) && axis_ray_ok(r.o, r.d);
-    // SLAB32 (PT_SLAB32, the FMA_SLAB builds): the planes' t in f32, t = fma(b, 1/d, -o/d), widened on each
-    // axis by e = 2^-21 (B + |o|) |1/d| (B >= every plane's |b|): against the real t = (b - o) / d, the f32
-    // 1/d and -o/d (each 2^-24 relative, after the f64 rounding), the fma's rounding and the widening's own
-    // rounding add up to less than 1.6 * 2^-23 (|b| + |o|) |1/d|, so the widened interval contains the real
-    // one and the cull stays conservative (1e-30 more covers an f32 flush of tiny values).  An axis whose
+    // SLAB32 (PT_SLAB32, the FMA_SLAB builds): the planes' t in f32, t = fma(b, 1/d, lo) for near planes and
+    // fma(b, 1/d, hi) for far ones, lo / hi = fl32(-o/d -/+ e), the widening e = 2^-21 (B + |o|) |1/d| (B >= every
+    // plane's |b|) folded into the offset in f64: against the real t = (b - o) / d, the f32 1/d and lo / hi
+    // (each one f32 rounding of the f64 value: 2^-24 relative) and the fma's rounding add up to less than
+    // 2^-23 ((|b| + |o|) |1/d| + e), so the widened interval contains the real one and the cull stays
+    // conservative (1e-30 more covers an f32 flush of tiny values).  The six FMAs run as three packed ones over
+    // the node's register pairs (nr0, nr1), (nr2, fr0), (fr1, fr2) (C5 +0.9 %, r4h).  An axis whose
     // 1/d or -o/d does not fit an f32 is left open (NaN t's drop out of fmax/fmin), and so is one whose |1/d| is
     // below 1e-30, where an f32 flush of b * 1/d could exceed the widening; min_t is rounded down and best up.
     // The hits are decided by the exact f64 leaf tests as in every walk.
     constexpr bool S32 = FMA_SLAB && PT_SLAB32;
-    auto axis32 = [&](double o, double iv, float *i32, float *m32, float *e32) {
+    auto axis32 = [&](double o, double iv, float *i32, float *lo32, float *hi32) {
         const double m = -(o * iv);
         const bool fits = fabs(iv) < 1e30 && fabs(iv) > 1e-30 && fabs(m) < 1e30;
+        const double e = (0x1p-21 * (1.0 + 0x1p-20)) * ((double)sc.bvh_bound + fabs(o)) * fabs(iv) + 1e-30;
         *i32 = (float)iv;
-        *m32 = fits ? (float)m : __builtin_nanf("");
-        *e32 = (float)((0x1p-21 * (1.0 + 0x1p-20)) * ((double)sc.bvh_bound + fabs(o)) * fabs(iv) + 1e-30);
+        *lo32 = fits ? (float)(m - e) : __builtin_nanf("");
+        *hi32 = fits ? (float)(m + e) : __builtin_nanf("");
     };
-    float ix = 0.f, iy = 0.f, iz = 0.f, mx32 = 0.f, my32 = 0.f, mz32 = 0.f, ex = 0.f, ey = 0.f, ez = 0.f;
+    float ix = 0.f, iy = 0.f, iz = 0.f, lox = 0.f, loy = 0.f, loz = 0.f, hix = 0.f, hiy = 0.f, hiz = 0.f;
     if (S32) {
-        axis32(r.o.x, inv.x, &ix, &mx32, &ex);
-        axis32(r.o.y, inv.y, &iy, &my32, &ey);
-        axis32(r.o.z, inv.z, &iz, &mz32, &ez);
+        axis32(r.o.x, inv.x, &ix, &lox, &hix);
+        axis32(r.o.y, inv.y, &iy, &loy, &hiy);
+        axis32(r.o.z, inv.z, &iz, &loz, &hiz);
     }
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v pa_i = {ix, iy}, pa_m = {lox, loy}, pb_i = {iz, ix}, pb_m = {loz, hix}, pc_i = {iy, iz},
+              pc_m = {hiy, hiz};
     const float mt32 = S32 ? (float)(min_t - fabs(min_t) * 0x1p-20) : 0.f;
     float best32 = S32 ? (float)(best + fabs(best) * 0x1p-20) : 0.f;
     int n = any && who >= 0 ? sc.nnodes : 0;
@@ -476,11 +482,10 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
         if (STATS) ct->c[C_NODE_SLABS]++;
         bool enter;
         if (S32) {
-            const float tn = fmaxf(fmaxf(__builtin_fmaf(nd.nr[0], ix, mx32) - ex, __builtin_fmaf(nd.nr[1], iy, my32) - ey),
-                                   fmaxf(__builtin_fmaf(nd.nr[2], iz, mz32) - ez, mt32));
-            const float tf = fminf(fminf(__builtin_fmaf(nd.fr[0], ix, mx32) + ex, __builtin_fmaf(nd.fr[1], iy, my32) + ey),
-                                   fminf(__builtin_fmaf(nd.fr[2], iz, mz32) + ez, best32));
-            enter = tn <= tf;
+            const f2v a = __builtin_elementwise_fma((f2v){nd.nr[0], nd.nr[1]}, pa_i, pa_m);
+            const f2v b = __builtin_elementwise_fma((f2v){nd.nr[2], nd.fr[0]}, pb_i, pb_m);
+            const f2v c = __builtin_elementwise_fma((f2v){nd.fr[1], nd.fr[2]}, pc_i, pc_m);
+            enter = fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, mt32)) <= fminf(fminf(b.y, c.x), fminf(c.y, best32));
         } else {
             const double tn = fmax(fmax(tx(nd.nr[0]), ty(nd.nr[1])), fmax(tz(nd.nr[2]), min_t));
             const double tf = fmin(fmin(tx(nd.fr[0]), ty(nd.fr[1])), fmin(tz(nd.fr[2]), best));

@@ -35,6 +35,8 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Msamples/sec cornell_box 1920x1080x256spp at 1/2/4/8 MI355X; RMS pixel delta"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (FMA = 2 FLOP); no-FMA instruction peak is half of it
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
+BIG_BVH_NODES = 1 << 15   # pt_types.hpp: from this many nodes per layout the bounce's node slab test is f32
 REF_THREADS = 12          # the reference GUI's ThreadPoolRenderer::new(scene, 12, 50) (src/bin/main.rs:229-239)
 
 # FLOPs per event of the kernels' own traversal (counted in pt_device.hpp /
@@ -58,6 +60,10 @@ FLOP_WEIGHTS = {
     "lambert": 20, "metal": 25, "dielectric": 40, "reject_tries": 14, "unwind": 3,
 }
 MARCH_EVENTS = ("test_march", "march_slabs", "march_steps", "march_tries", "march_blocks")
+
+
+def kt_src_has_bounce(src):
+    return src.get("bounce", (0, 0))[1] > 0
 
 
 def flops_per_sample(cnt, keys=None):
@@ -437,6 +443,19 @@ def main():
                                         "flops_per_sample_weights": round(f_weights[k], 1), "launches": n_k // nfr,
                                         "ms_per_frame": round(ms_k / nfr, 3),
                                         "kernel_ms_avg": round(ms_k / n_k, 4)}
+        # the large-tree bounce build tests BVH nodes in f32: 6 FMAs per node slab, outside the f64
+        # counters; reported beside the f64 roofline, and both shares of the VALU's FLOP rate summed
+        f32_kind = {}
+        if r.get_option("bvh_nodes") >= BIG_BVH_NODES and kt_src_has_bounce(src):
+            f32_ps = 12.0 * counts["node_slabs"] / max(1, counts["samples"])
+            ms_b, _ = src["bounce"]
+            a32 = f32_ps * samples_share * nfr / (ms_b / 1e3) / 1e12
+            f32_kind = {"kernel": "wf_bounce", "flops_per_sample": round(f32_ps, 1), "achieved": round(a32, 4),
+                        "peak": FP32_PEAK_TFLOPS, "frac": round(a32 / FP32_PEAK_TFLOPS, 5),
+                        "source": "node_slabs events (pt_count_work) x 12 (six f32 FMAs per node)"}
+            if "wf_bounce" in per_kernel:
+                per_kernel["wf_bounce"]["valu_frac_f64_plus_f32"] = round(
+                    per_kernel["wf_bounce"]["frac"] + a32 / FP32_PEAK_TFLOPS, 5)
         out_bytes = 24.0 * W * H * share
         tuning = {k: v for k, v in r.options().items() if v != pt.OPTION_DEFAULTS.get(k)}
         rec = {
@@ -459,6 +478,7 @@ def main():
                                       "every launch alone on the device, HIP events on its stream"
                                       if kt_iso is not None else "timed steps (launches of two chunk streams overlap)"),
                          "kernels": per_kernel,
+                         "valu_f32": f32_kind or None,
                          "flops_per_sample_total": round(F, 1),
                          "flops_source": ("f64 instruction counters x mean active lanes, %s (%s; scripts/pmc_flops.py); "
                                           "event weights give %.1f FLOP/sample (%.2fx)"

@@ -163,12 +163,13 @@ int pt_renderer_peer_access(const pt_renderer *r, int *pairs, int *enabled);
  * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
  * "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
  * "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "bvh_leaf" (shapes
- * per BVH leaf: setting it rebuilds the BVH on every device).  A new renderer takes them from the PT_*
- * environment variables (PT_ENGINE=mega|wave, PT_WAVES, PT_WF_SLOTS, ...)
- * once; set_option changes them for every device of the renderer (not while
- * a render_start frame is in flight).  No knob changes the image: every
- * setting renders the same bits.  pt_option_name(i) lists the names (NULL
- * past the end). */
+ * per BVH leaf: setting it rebuilds the BVH on every device).  A new renderer
+ * starts from the defaults; set_option changes them for every device of the
+ * renderer (not while a render_start frame is in flight).  No knob changes the
+ * image: every setting renders the same bits.  pt_option_name(i) lists the
+ * names (NULL past the end).  get_option also reads "bvh_nodes" (read-only:
+ * nodes per octant layout of the renderer's BVH; from 32768 on, the bounce
+ * runs its large-tree build, whose node slab test is f32). */
 int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value);
 int pt_renderer_get_option(const pt_renderer *r, const char *name, int64_t *value);
 const char *pt_option_name(int index);

@@ -724,6 +724,10 @@ int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
 
 int pt_renderer_get_option(const pt_renderer *r, const char *name, int64_t *value) {
     if (!r || !name || !value) return fail(PT_ERR_INVALID, "null argument");
+    if (!std::strcmp(name, "bvh_nodes")) {  // read-only state
+        *value = r->gpus[0].ds.nnodes;
+        return PT_OK;
+    }
     if (tuning_get(r->gpus[0].ws.tune, name, value) != PT_OK) return fail(PT_ERR_INVALID, std::string("unknown option: ") + name);
     return PT_OK;
 }

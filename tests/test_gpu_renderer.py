@@ -376,3 +376,20 @@ def test_plain_c_caller_renders_through_the_abi(pt, cornell_text):
         img = np.fromfile(out, dtype=np.float64).reshape(-1, 3)
     ref = O.Scene(cornell_text, seed=1).render(w, h, spp, 8, 5, threads=host_threads())
     assert np.array_equal(img, ref)
+
+
+def test_bvh_nodes_is_read_only_state(pt, cornell):
+    """get_option("bvh_nodes"): nodes per octant layout (bench.py picks the f32 node-slab accounting from it);
+    not a tuning knob, so set_option refuses it and options() does not list it."""
+    ps, _ = cornell
+    r = pt.HipRenderer(ps, depth=8)
+    n = r.get_option("bvh_nodes")
+    assert 0 < n < 1 << 15  # cornell's ~480 random spheres: the small-tree builds
+    with pytest.raises(pt.PtError):
+        r.set_option("bvh_nodes", 5)
+    assert "bvh_nodes" not in r.options()
+    leaf0 = r.get_option("bvh_leaf")
+    r.set_option("bvh_leaf", 2)  # two shapes per leaf: fewer nodes
+    assert r.get_option("bvh_nodes") < n
+    r.set_option("bvh_leaf", leaf0)
+    assert r.get_option("bvh_nodes") == n

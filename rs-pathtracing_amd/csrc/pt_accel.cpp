@@ -124,6 +124,71 @@ struct Builder {
         int axis = 0;
         for (int k = 1; k < 3; k++)
             if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+        // Binned surface-area split: 32 bins per axis over the centroid bounds, the cut that minimises
+        // n_left * area(left) + n_right * area(right) (C5 node tests per sample 127.6 -> 120.6, 1568 -> 1635 M
+        // samples/s; 8 / 64 / 128 bins: 121.7 / 120.0 / 120.6 on the host count); the median split on the widest
+        // centroid axis when no cut separates the boxes.  Any tree gives the same hits: the acceptance rule is
+        // order-independent.
+        if (b - a > 2) {
+            constexpr int NB = 32;
+            auto area = [](const double *lo, const double *hi) {
+                const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+                return x * y + y * z + z * x;
+            };
+            double best = INFINITY;
+            int bk = -1, bi = -1;
+            for (int k = 0; k < 3; k++) {
+                const double ext = chi[k] - clo[k];
+                if (!(ext > 0.0)) continue;
+                int cnt[NB] = {};
+                double blo[NB][3], bhi[NB][3];
+                for (int j = 0; j < NB; j++)
+                    for (int r = 0; r < 3; r++) blo[j][r] = INFINITY, bhi[j][r] = -INFINITY;
+                for (size_t i = a; i < b; i++) {
+                    const DBox &x = boxes[ids[i]];
+                    int j = (int)((0.5 * (x.lo[k] + x.hi[k]) - clo[k]) / ext * NB);
+                    j = j < 0 ? 0 : (j >= NB ? NB - 1 : j);
+                    cnt[j]++;
+                    for (int r = 0; r < 3; r++) blo[j][r] = std::min(blo[j][r], x.lo[r]), bhi[j][r] = std::max(bhi[j][r], x.hi[r]);
+                }
+                double rlo[NB][3], rhi[NB][3];
+                int rc[NB];
+                for (int j = NB - 1; j >= 0; j--) {
+                    for (int r = 0; r < 3; r++) {
+                        rlo[j][r] = j + 1 < NB ? std::min(rlo[j + 1][r], blo[j][r]) : blo[j][r];
+                        rhi[j][r] = j + 1 < NB ? std::max(rhi[j + 1][r], bhi[j][r]) : bhi[j][r];
+                    }
+                    rc[j] = (j + 1 < NB ? rc[j + 1] : 0) + cnt[j];
+                }
+                double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                int lc = 0;
+                for (int j = 0; j + 1 < NB; j++) {
+                    lc += cnt[j];
+                    for (int r = 0; r < 3; r++) llo[r] = std::min(llo[r], blo[j][r]), lhi[r] = std::max(lhi[r], bhi[j][r]);
+                    if (lc == 0 || rc[j + 1] == 0) continue;
+                    const double c = lc * area(llo, lhi) + rc[j + 1] * area(rlo[j + 1], rhi[j + 1]);
+                    if (c < best) best = c, bk = k, bi = j;
+                }
+            }
+            if (bk >= 0) {
+                const double ext = chi[bk] - clo[bk];
+                auto left = [&](int32_t id) {
+                    const DBox &x = boxes[id];
+                    int j = (int)((0.5 * (x.lo[bk] + x.hi[bk]) - clo[bk]) / ext * NB);
+                    j = j < 0 ? 0 : (j >= NB ? NB - 1 : j);
+                    return j <= bi;
+                };
+                const size_t m = (size_t)(std::stable_partition(ids.begin() + a, ids.begin() + b, left) - ids.begin());
+                if (m > a && m < b) {
+                    const int l = emit(ids, a, m);
+                    const int r = emit(ids, m, b);
+                    n.count = 0;
+                    n.first = 0;
+                    tree[me] = TNode{n, bk, l, r};
+                    return me;
+                }
+            }
+        }
         size_t mid = a + (b - a) / 2;
         std::nth_element(ids.begin() + a, ids.begin() + mid, ids.begin() + b, [&](int32_t x, int32_t y) {
             double cx = boxes[x].lo[axis] + boxes[x].hi[axis], cy = boxes[y].lo[axis] + boxes[y].hi[axis];

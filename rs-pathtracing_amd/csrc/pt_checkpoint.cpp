@@ -13,6 +13,7 @@
 // Layout (little-endian): "PTCKPT01", the pt_checkpoint header (56 bytes),
 // count doubles, and a 64-bit FNV-1a checksum over everything before it taken
 // as 64-bit words (word-wise, so a 200 MB 4K frame checks at memory speed).
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -59,6 +60,7 @@ const char *header_problem(const pt_checkpoint &c) {
 }
 
 thread_local std::string g_ck_err;
+std::atomic<unsigned long> g_tmp_seq{0};  // distinct temporaries for saves from several threads
 
 }  // namespace
 
@@ -77,7 +79,8 @@ int pt_checkpoint_save(const char *path, const pt_checkpoint *c, const double *s
     if (!path || !c || !sums) return ck_fail(PT_ERR_INVALID, "pt_checkpoint_save: null argument");
     if (const char *why = header_problem(*c)) return ck_fail(PT_ERR_INVALID, std::string("pt_checkpoint_save: ") + why);
     // a temporary next to the target, renamed over it once complete: a crash mid-write leaves the old file
-    const std::string tmp = std::string(path) + ".tmp." + std::to_string((long)getpid());
+    const std::string tmp = std::string(path) + ".tmp." + std::to_string((long)getpid()) + "." +
+                            std::to_string(g_tmp_seq.fetch_add(1));
     FILE *f = std::fopen(tmp.c_str(), "wb");
     if (!f) return ck_fail(PT_ERR_IO, "pt_checkpoint_save: cannot open " + tmp + " for writing");
     uint64_t h = fnv_words(kFnvOffset, kMagic, 1);

@@ -121,3 +121,28 @@ def test_invalid_windows(pt, cornell):
         with pytest.raises(pt.PtError) as e:
             r.render_device_samples(cam, 64, 32, 8, 1, 0, 1, a, b, out.data_ptr())
         assert e.value.code == pt.PT_ERR_INVALID
+
+
+def test_cli_render_interrupted_and_resumed(tmp_path):
+    """tools/pt_render (the headless CLI over the C-ABI): a frame stopped after its first window (-x 1, exit 3,
+    checkpoint kept) and resumed by a second process equals the frame rendered in one go, bit for bit; the
+    checkpoint is removed when the frame completes, and the image is a PNG."""
+    import subprocess
+    exe = str(ROOT / "tools" / "pt_render")
+    scene = str(ROOT / "scenes" / "cornell_box.json")
+    args = [exe, scene, "12", "96", "64", "-d", "8", "-s", "3"]
+    one = subprocess.run(args + ["-f", str(tmp_path / "one.f64"), "-o", str(tmp_path / "one.png")],
+                         capture_output=True, text=True, timeout=120)
+    assert one.returncode == 0, one.stderr
+    ck = tmp_path / "frame.ckpt"
+    first = subprocess.run(args + ["-c", str(ck), "-n", "5", "-x", "1", "-o", ""], capture_output=True, text=True,
+                           timeout=120)
+    assert first.returncode == 3, first.stderr
+    assert ck.exists()
+    second = subprocess.run(args + ["-c", str(ck), "-n", "5", "-f", str(tmp_path / "res.f64"), "-o", ""],
+                            capture_output=True, text=True, timeout=120)
+    assert second.returncode == 0, second.stderr
+    assert "resuming at sample 5 of 12" in second.stderr
+    assert not ck.exists()
+    assert (tmp_path / "one.f64").read_bytes() == (tmp_path / "res.f64").read_bytes()
+    assert (tmp_path / "one.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"

@@ -135,3 +135,12 @@ def test_committed_passes_serve_every_cornell_config():
             f2, rec2, _, why = bench.pmc_lookup(f.name.split("_")[1], "cornell_box.json", 8, 3840, 2160, 4096,
                                                 rec["source_id"])
             assert rec2 is not None and rec2["source_id"] == rec["source_id"], why
+
+
+def test_f32_node_flops_per_sample():
+    """The large-tree bounce's f32 node work for the roofline's valu_f32 part: 12 FLOPs per node test, less the
+    root test its walk skips once per trace (C5 host count: 120.6 node tests and 2.73 traces per sample)."""
+    import bench
+    counts = {"samples": 1000, "node_slabs": 120596, "bounces": 2731}
+    assert abs(bench.f32_node_flops_per_sample(counts) - 12 * (120596 - 2731) / 1000) < 1e-9
+    assert bench.f32_node_flops_per_sample({"samples": 0, "node_slabs": 0, "bounces": 0}) == 0.0

@@ -4,6 +4,15 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
     python bench.py --gpus N --single-process      # N devices behind one pt_renderer_create_multi
 
+A plain `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment)
+starts `python -m torch.distributed.run --nproc-per-node N ... bench.py ...`
+as a child process (this process never touches the GPU) and exits with its
+exit code; rank 0 prints the JSON line.  With the nccl backend and fewer than
+N visible devices it exits non-zero, naming the device count: one rank per GPU
+(the reference's parallelism knob takes effect however the renderer is
+started, ThreadPoolRenderer::new(scene, thread_number, depth),
+src/renderer/step_by_step.rs:37).
+
 One step = one full frame (all W*H*spp camera samples, every bounce) rendered
 from scene data resident in HBM into an HBM frame buffer.  For N > 1 the
 frame's 16x16 tiles are dealt round-robin to the ranks (tile k -> rank k % N),
@@ -130,6 +139,50 @@ def parse():
     if a.config:
         a.scene, a.width, a.height, a.spp = CONFIGS[a.config]
     return a
+
+
+def launch_plan(args, env):
+    """How this invocation runs: "ranks" (it is a rank of a torch.distributed launch: WORLD_SIZE is set),
+    "spawn" (--gpus N > 1 with no launcher: start one as a child), "single-process" (N devices behind one
+    pt_renderer_create_multi) or "one" (one GPU)."""
+    if "WORLD_SIZE" in env:
+        return "ranks"
+    if args.gpus > 1:
+        return "single-process" if args.single_process else "spawn"
+    return "one"
+
+
+def device_shortfall(world, backend, ndev):
+    """The error for `world` ranks on `ndev` visible devices, or None: RCCL needs one GPU per rank; gloo ranks may
+    share one (a rehearsal of the rank path)."""
+    if backend == "nccl" and world > ndev:
+        return ("bench.py: %d ranks over nccl (RCCL) need %d GPUs, but %d device%s visible"
+                % (world, world, ndev, " is" if ndev == 1 else "s are"))
+    if ndev < 1:
+        return "bench.py: no GPU visible"
+    return None
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv):
+    """Runs this bench as N ranks under torch.distributed.run in a child process (no exec: this process has not
+    touched the GPU, and the child is a new program) and returns the child's exit code."""
+    import subprocess
+    import torch
+    err = device_shortfall(args.gpus, args.dist_backend, torch.cuda.device_count())  # counting does not init HIP
+    if err:
+        print(err, file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py")] + list(argv)
+    print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
 
 
 def metric_name(args):
@@ -278,6 +331,8 @@ def pmc_lookup(what, scene, depth, width, height, spp, source, root=ROOT):
 
 def main():
     args = parse()
+    if launch_plan(args, os.environ) == "spawn":
+        sys.exit(spawn_ranks(args, sys.argv[1:]))
     if os.environ.get("PT_SEGV_LOG"):  # diagnostics: a host fault's address, registers and mappings to a file
         import ctypes
         ctypes.CDLL(str(ROOT / "tools" / "segv_maps.so")).pt_segv_install(os.environ["PT_SEGV_LOG"].encode())
@@ -292,6 +347,11 @@ def main():
     if world != args.gpus and rank == 0 and not multi:
         print("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     gloo = world > 1 and args.dist_backend == "gloo"
+    err = device_shortfall(world, args.dist_backend, torch.cuda.device_count()) if world > 1 else None
+    if err:
+        if rank == 0:
+            print(err, file=sys.stderr, flush=True)
+        sys.exit(2)
     if gloo:  # rehearsal of the multi-rank path on fewer GPUs than ranks
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)

@@ -71,20 +71,24 @@ typedef int (*pt_image_loader)(void *user, const char *filename, uint32_t *width
  * no byte at or past opts + struct_size.  A caller sets struct_size =
  * sizeof(pt_scene_opts) of the header it was compiled against (or uses
  * PT_SCENE_OPTS_INIT).  struct_size == 0 is a caller built against 0.1.0 or
- * 0.2.0, where this field was `reserved` (always 0) and the struct already had
- * this 32-byte layout: every field is read, load_image and image_user
- * included.  A size between 1 and 15 is rejected (PT_ERR_INVALID); a size of
- * 16 to 31 reads only the fields it covers (16: no loader); fields a newer
- * caller appends past sizeof(pt_scene_opts) are ignored. */
+ * 0.2.0, where this field was `reserved` (always 0): 0.1.0's struct was the 16
+ * bytes {random_spheres, reserved, seed}, 0.2.0's added load_image and
+ * image_user, and a 0 cannot tell the two apart, so 0 reads the 16 bytes both
+ * have and never a loader (ABI version 4; a 0.2.0 caller's ImageTexture files
+ * then go to the built-in PPM reader).  An image loader is used only with a
+ * struct_size that covers it.  A size between 1 and 15 is rejected
+ * (PT_ERR_INVALID); a size of 16 to 31 reads only the fields it covers (16: no
+ * loader); fields a newer caller appends past sizeof(pt_scene_opts) are
+ * ignored. */
 typedef struct {
     uint32_t random_spheres; /* 1 = reference behaviour (default), 0 = JSON shapes only */
-    uint32_t struct_size;    /* sizeof(pt_scene_opts); 0 = a 0.1.0 / 0.2.0 caller's struct of this layout */
+    uint32_t struct_size;    /* sizeof(pt_scene_opts); 0 = a 0.1.0 / 0.2.0 caller: its first 16 bytes only */
     uint64_t seed; /* seed of the add_random_spheres stream and of the NoiseTexture Perlin tables */
     pt_image_loader load_image; /* NULL: built-in PPM reader (read only if struct_size covers it) */
     void *image_user;
 } pt_scene_opts;
 #define PT_SCENE_OPTS_MIN_SIZE 16    /* {random_spheres, struct_size, seed} */
-#define PT_SCENE_OPTS_LEGACY_SIZE 32 /* what struct_size == 0 means: the 0.1.0 / 0.2.0 struct */
+#define PT_SCENE_OPTS_LEGACY_SIZE 16 /* what struct_size == 0 means: the bytes 0.1.0 and 0.2.0 structs share */
 #define PT_SCENE_OPTS_INIT {1u, (uint32_t)sizeof(pt_scene_opts), 1u, NULL, NULL}
 
 /* Camera (src/camera/mod.rs:36-46).  fov in radians, as Camera::new takes it. */
@@ -259,8 +263,9 @@ typedef struct pt_checkpoint {
     uint64_t scene_key;
     uint64_t count; /* doubles of sums: width*height*3 (world 1) or pt_shard_tiles(...)*768 */
 } pt_checkpoint;
-/* Writes header + sums[0..count) to path (atomically: a temporary file renamed
- * over it).  The header must be consistent (samples_done <= samples_number,
+/* Writes header + sums[0..count) to path (atomically: a temporary file, synced
+ * to disk, renamed over it, then the directory synced, so a crash or a power
+ * loss leaves the old file or the new one).  The header must be consistent (samples_done <= samples_number,
  * rank < world, count as above), else PT_ERR_INVALID. */
 int pt_checkpoint_save(const char *path, const pt_checkpoint *c, const double *sums);
 /* Reads path's header into *c and, when sums is not NULL, its count sums
@@ -315,6 +320,17 @@ int pt_march_jobs(pt_renderer *r, const double *jobs, size_t n, double *t_out, i
  * PT_ERR_STATE while a render_start frame is in flight. */
 int pt_march_guard_drops(pt_renderer *r, uint64_t *count);
 
+/* What pt_render_stop did on the devices since the last call (read and
+ * cleared, summed over the renderer's devices): *skipped = launches of the
+ * stop-gated paths (wavefront bounce, march and sample-reduce launches,
+ * megakernel blocks) that found their frame stopped and did nothing;
+ * *worked = launches that found it stopped and still had work (0 unless the
+ * gate is broken: every launch queued behind a fired gate must be a no-op).
+ * The mechanism behind stop_rendering's latency (step_by_step.rs:73-77: the
+ * workers check a flag between chunks).  Waits for the devices; PT_ERR_STATE
+ * while a render_start frame is in flight. */
+int pt_render_stop_stats(pt_renderer *r, uint64_t *skipped, uint64_t *worked);
+
 /* Per-kernel launch timing of the render path (bench / roofline): returns
  * the summed HIP-event durations (ms) and launch counts per kernel kind since
  * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
@@ -364,10 +380,11 @@ const char *pt_version(void);
 
 /* ---- ABI self-description ----------------------------------------------- */
 /* PT_ABI_VERSION changes whenever an entry point's signature or a struct's
- * layout changes (3: pt_scene_opts.struct_size, pt_unshard_device's leading
- * `device`, pt_abi_layout).  A binding compares it with the value it was
+ * layout or meaning changes (3: pt_scene_opts.struct_size, pt_unshard_device's
+ * leading `device`, pt_abi_layout; 4: struct_size 0 reads 16 bytes, no
+ * loader).  A binding compares it with the value it was
  * written for before calling anything else. */
-#define PT_ABI_VERSION 3
+#define PT_ABI_VERSION 4
 uint32_t pt_abi_version(void);
 /* Layout of a boundary struct as the library was compiled: out[0] = sizeof,
  * out[1 + k] = offsetof of the k-th field in declaration order.  Writes

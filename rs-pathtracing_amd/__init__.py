@@ -45,12 +45,12 @@ EXPORTS = [
     "pt_renderer_set_option", "pt_renderer_get_option", "pt_option_name",
     "pt_render_start", "pt_render_step", "pt_render_step_rgba8", "pt_render_stop",
     "pt_render_device", "pt_render_frame_device", "pt_shard_tiles", "pt_unshard_device", "pt_closest_hit",
-    "pt_ray_color", "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_march_guard_drops", "pt_wave_diag",
+    "pt_ray_color", "pt_trace_pixel_samples", "pt_count_work", "pt_profile_phases", "pt_march_jobs", "pt_march_guard_drops", "pt_render_stop_stats", "pt_wave_diag",
     "pt_kernel_timing", "pt_encode_rgba8", "pt_encode_rgba8_device", "pt_write_png", "pt_write_ppm",
     "pt_sample_key", "pt_last_error", "pt_version", "pt_abi_version", "pt_abi_layout", "pt_renderer_peer_access",
     "pt_render_device_samples", "pt_checkpoint_save", "pt_checkpoint_load",
 ]
-ABI_VERSION = 3  # PT_ABI_VERSION this binding is written for
+ABI_VERSION = 4  # PT_ABI_VERSION this binding is written for
 
 
 class PtError(RuntimeError):
@@ -167,6 +167,7 @@ def lib():
                                     C.POINTER(C.c_uint32)]),
         "pt_kernel_timing": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(u32), sz]),
         "pt_march_guard_drops": (C.c_int, [vp, C.POINTER(u64)]),
+        "pt_render_stop_stats": (C.c_int, [vp, C.POINTER(u64), C.POINTER(u64)]),
         "pt_wave_diag": (C.c_int, [vp, C.c_int, C.POINTER(u64), sz]),
         "pt_profile_phases": (C.c_int, [vp, C.POINTER(CameraStruct), u32, u32, u32, u64, C.POINTER(u64)]),
         "pt_encode_rgba8": (C.c_int, [d, sz, C.POINTER(C.c_uint8)]),
@@ -471,6 +472,14 @@ def march_guard_drops(renderer: "HipRenderer") -> int:
     n = C.c_uint64()
     _check(lib().pt_march_guard_drops(renderer._h, C.byref(n)))
     return n.value
+
+
+def render_stop_stats(renderer: "HipRenderer"):
+    """(skipped, worked) since the last call (pt_render_stop_stats): stop-gated launches that found their frame
+    stopped, and those of them that still had work (0 unless the stop gate is broken)."""
+    s, w = C.c_uint64(), C.c_uint64()
+    _check(lib().pt_render_stop_stats(renderer._h, C.byref(s), C.byref(w)))
+    return s.value, w.value
 
 
 def march_jobs(renderer: "HipRenderer", jobs, status=False):

@@ -91,6 +91,7 @@ struct pt_renderer {
     double *d_gather = nullptr;  // multi-device: world shards back to back, on gpus[0]
     size_t gather_cap = 0;
     int peer_pairs = 0, peer_enabled = 0;  // distinct (gpus[0], gpus[k]) device pairs; with peer access both ways
+    int fault_accel_alloc = 0;  // test hook (option "fault_accel_alloc"): this renderer's next BVH rebuild fails
     // A progressive frame is a list of bands of tile rows.  A feeder thread
     // queues them on the device(s), keeping two bands ahead of the GPU (one
     // running, one queued), so the device never idles between bands and
@@ -128,7 +129,7 @@ __attribute__((visibility("hidden"))) void pt_set_last_error(const char *msg) { 
 #define PT_SRC_SHA "unknown"
 #endif
 const char *pt_version(void) {
-    return "rs-pathtracing-amd 0.3.0 (gfx950, f64 megakernel + wavefront march engine; src " PT_SRC_SHA ")";
+    return "rs-pathtracing-amd 0.4.0 (gfx950, f64 megakernel + wavefront march engine; src " PT_SRC_SHA ")";
 }
 uint32_t pt_abi_version(void) { return PT_ABI_VERSION; }
 
@@ -188,9 +189,9 @@ int pt_scene_create_from_json(const char *json, size_t len, const pt_scene_opts 
     if (!json || !out) return fail(PT_ERR_INVALID, "null argument");
     *out = nullptr;
     // struct_size versions the options (header): no byte at or past
-    // opts + struct_size is read; 0 is a 0.1.0 / 0.2.0 caller, whose struct
-    // (with `reserved` = 0 in this field) already had the 32-byte layout and
-    // its image loader
+    // opts + struct_size is read; 0 is a 0.1.0 (16-byte struct) or 0.2.0
+    // (32-byte) caller with `reserved` = 0 in this field, which 0 cannot tell
+    // apart, so only the 16 bytes both have are read (no image loader)
     const size_t osz = !opts ? 0 : (opts->struct_size ? opts->struct_size : (size_t)PT_SCENE_OPTS_LEGACY_SIZE);
     if (opts && osz < PT_SCENE_OPTS_MIN_SIZE)
         return fail(PT_ERR_INVALID, "pt_scene_opts.struct_size " + std::to_string(osz) +
@@ -316,9 +317,10 @@ struct StagedAccel {
     float bvh_bound = 0.f;
 };
 
-// Test hook (renderer option "fault_accel_alloc" = n): the n-th device
-// allocation of the next BVH rebuild fails as if the device were out of memory.
-std::atomic<int> g_fault_accel_alloc{0};
+// Test hook (renderer option "fault_accel_alloc" = n, kept per renderer): the
+// n-th device allocation of that renderer's next BVH rebuild fails as if the
+// device were out of memory.  `fault` is the renderer's counter (null when
+// creating a renderer: no hook).
 
 void free_staged(int device, StagedAccel &a) {
     (void)hipSetDevice(device);
@@ -328,14 +330,13 @@ void free_staged(int device, StagedAccel &a) {
     a = StagedAccel{};
 }
 
-int stage_accel(int device, const Accel &acc, StagedAccel *out) {
+int stage_accel(int device, const Accel &acc, StagedAccel *out, int *fault = nullptr) {
     StagedAccel a;
     hipError_t err = hipSetDevice(device);
-    auto upload = [&err](auto **dst, const auto &vec) {
+    auto upload = [&err, fault](auto **dst, const auto &vec) {
         using T = typename std::remove_reference<decltype(vec)>::type::value_type;
         size_t n = vec.empty() ? 1 : vec.size();
-        if (err == hipSuccess && g_fault_accel_alloc.load() > 0 && g_fault_accel_alloc.fetch_sub(1) == 1)
-            err = hipErrorOutOfMemory;
+        if (err == hipSuccess && fault && *fault > 0 && (*fault)-- == 1) err = hipErrorOutOfMemory;
         if (err == hipSuccess) err = hipMalloc((void **)dst, n * sizeof(T));
         if (err == hipSuccess && !vec.empty())
             err = hipMemcpy(*dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice);
@@ -400,8 +401,10 @@ int init_share(GpuShare &g, int device, const Scene &S, const Accel &acc, const 
         upload(&g.ds.pixels, S.pixels);
     }
     if (err == hipSuccess) err = hipEventCreateWithFlags(&g.shard_ev, hipEventDisableTiming);
-    if (err == hipSuccess) err = hipMalloc((void **)&g.ds.guard, sizeof(unsigned long long));
-    if (err == hipSuccess) err = hipMemset(g.ds.guard, 0, sizeof(unsigned long long));
+    // device counters: [0] march guard drops, [1] stop-gated launches that found the frame stopped, [2] of those,
+    // launches that still had work (pt_render_stop_stats)
+    if (err == hipSuccess) err = hipMalloc((void **)&g.ds.guard, 4 * sizeof(unsigned long long));
+    if (err == hipSuccess) err = hipMemset(g.ds.guard, 0, 4 * sizeof(unsigned long long));
     if (err != hipSuccess) return hip_fail(err, "uploading the scene");
     StagedAccel a;
     if (int rc = stage_accel(device, acc, &a)) return rc;
@@ -689,7 +692,7 @@ int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
             const Accel acc = build_accel(r->scene->s, r->scene->s.json_shapes, t.bvh_leaf);
             // every device stages the new tree before any device lets go of the old one
             for (size_t k = 0; k < r->gpus.size(); k++)
-                if (int rc = stage_accel(r->gpus[k].device, acc, &staged[k])) {
+                if (int rc = stage_accel(r->gpus[k].device, acc, &staged[k], &r->fault_accel_alloc)) {
                     drop();
                     return rc;
                 }
@@ -703,9 +706,9 @@ int pt_renderer_set_option(pt_renderer *r, const char *name, int64_t value) {
                 return rc;
             }
     }
-    if (!std::strcmp(name, "fault_accel_alloc")) {  // test hook, see g_fault_accel_alloc
+    if (!std::strcmp(name, "fault_accel_alloc")) {  // test hook of this renderer, see stage_accel
         if (value < 0 || value > 64) return fail(PT_ERR_INVALID, "fault_accel_alloc out of range (0..64)");
-        g_fault_accel_alloc.store((int)value);
+        r->fault_accel_alloc = (int)value;
         return PT_OK;
     }
     for (auto &g : r->gpus) {
@@ -1062,6 +1065,24 @@ int pt_march_guard_drops(pt_renderer *r, uint64_t *count) {
         total += n;
     }
     *count = total;
+    return PT_OK;
+}
+
+int pt_render_stop_stats(pt_renderer *r, uint64_t *skipped, uint64_t *worked) {
+    if (!r || !skipped || !worked) return fail(PT_ERR_INVALID, "null argument");
+    if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
+    uint64_t s = 0, w = 0;
+    for (auto &g : r->gpus) {
+        HIP_TRY(hipSetDevice(g.device));
+        HIP_TRY(hipDeviceSynchronize());
+        unsigned long long c[2] = {0, 0};
+        HIP_TRY(hipMemcpy(c, g.ds.guard + 1, sizeof c, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(g.ds.guard + 1, 0, sizeof c));
+        s += c[0];
+        w += c[1];
+    }
+    *skipped = s;
+    *worked = w;
     return PT_OK;
 }
 

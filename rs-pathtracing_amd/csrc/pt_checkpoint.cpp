@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
 #include <unistd.h>
 
 #include "../../include/rs_pathtracing.h"
@@ -88,11 +89,23 @@ int pt_checkpoint_save(const char *path, const pt_checkpoint *c, const double *s
     h = fnv_words(h, sums, c->count);
     bool ok = std::fwrite(kMagic, 1, 8, f) == 8 && std::fwrite(c, sizeof *c, 1, f) == 1 &&
               std::fwrite(sums, 8, c->count, f) == c->count && std::fwrite(&h, 8, 1, f) == 1;
+    // durable before it replaces the target: the data reaches the disk before the rename, and the rename
+    // (the directory entry) before the call returns, so a power loss leaves the old checkpoint or the new one
+    ok = ok && std::fflush(f) == 0 && ::fsync(fileno(f)) == 0;
     ok = (std::fclose(f) == 0) && ok;
     if (!ok || std::rename(tmp.c_str(), path) != 0) {
         std::remove(tmp.c_str());
         return ck_fail(PT_ERR_IO, std::string("pt_checkpoint_save: short write to ") + path);
     }
+    std::string dir(path);
+    const size_t slash = dir.find_last_of('/');
+    dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : dir.substr(0, slash));
+    const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+    if (dfd < 0 || ::fsync(dfd) != 0) {
+        if (dfd >= 0) ::close(dfd);
+        return ck_fail(PT_ERR_IO, "pt_checkpoint_save: cannot sync the directory of " + std::string(path));
+    }
+    ::close(dfd);
     return PT_OK;
 }
 

@@ -198,6 +198,19 @@ PT_HD void note_guard(unsigned long long *guard) {
 #endif
 }
 
+// A stop-gated launch that found its frame stopped (pt_render_stop_stats): counters[1] counts them, counters[2]
+// those that still had work to do (0 unless the stop gate failed to empty the queue).
+PT_HD void note_stop(unsigned long long *counters, bool worked) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!counters) return;
+    atomicAdd(counters + 1, 1ull);
+    if (worked) atomicAdd(counters + 2, 1ull);
+#else
+    (void)counters;
+    (void)worked;
+#endif
+}
+
 // MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
 // every one on the march list), so the march branch is not compiled in.
 // EXT: the extended build (scenes with a Torus or non-solid textures) that

@@ -29,7 +29,10 @@ template <int NW, int WAVES, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, WAVES) void render_tiles(dev::Scene sc, FrameParams P, double *__restrict__ out) {
     if (P.stop) {  // progressive frames: one read of the host-mapped stop flag per block
         __shared__ int halt;
-        if (threadIdx.x == 0) halt = dev::stopped(P.stop);
+        if (threadIdx.x == 0) {
+            halt = dev::stopped(P.stop);
+            if (halt) dev::note_stop(sc.guard, false);
+        }
         __syncthreads();
         if (halt) return;
     }

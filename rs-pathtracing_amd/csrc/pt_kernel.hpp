@@ -78,6 +78,12 @@ struct WaveWorkspace {
     // the next frame (on any stream) waits for it
     hipEvent_t done = nullptr;
     bool used = false;
+    // the launches' argument blocks of the last frame (pt_wave.hip WfArgs): pinned staging and device copy;
+    // args_ev is recorded after the frame's copy (the staging buffer is free once it has run)
+    void *args_host = nullptr, *args_dev = nullptr;
+    size_t args_bytes = 0;
+    hipEvent_t args_ev = nullptr;
+    bool args_pending = false;
     int device = -1;
     int side_priority = 0;  // the priority the side streams were created with (Tuning::wf_side_priority)
 };

@@ -55,23 +55,30 @@ using dev::V3;
 // alternate by iteration), so every later kernel reads a dense, id-ordered
 // subsequence of the previous bounce's outputs instead of a sparse one of the
 // chunk's slots.  The slot id (sample, pixel) travels with the path.
-// One base pointer and the slot count (not 11 pointers): the kernels' two
-// sets would otherwise hold 44 SGPRs of addresses.
+// Blocks of 64 positions (one wave's worth), each field a contiguous run in
+// the block: the eight 8-byte fields (ray, best hit t, rng) at 512-byte steps,
+// then the three 4-byte ones (who, meta, slot id) at 256-byte steps, 4864 B
+// per block.  A wave on 64 consecutive positions reads or writes each field
+// as one 512- (256-) byte run, as in plain structure of arrays, but every
+// field sits at an immediate offset from one per-lane address: with one array
+// per field the loop-invariant field bases of the two sets were 22 SGPR pairs,
+// and the bounce kernel spilled 65 SGPRs to VGPR lanes (round 5).
 struct PathSoA {
     char *base;
-    size_t cap;
+    size_t cap;  // a multiple of 64
     static constexpr size_t BYTES = 8 * 8 + 3 * 4;  // per path
-    __host__ __device__ double *ox() const { return (double *)base; }  // ray, best hit t
-    __host__ __device__ double *oy() const { return (double *)base + cap; }
-    __host__ __device__ double *oz() const { return (double *)base + 2 * cap; }
-    __host__ __device__ double *dx() const { return (double *)base + 3 * cap; }
-    __host__ __device__ double *dy() const { return (double *)base + 4 * cap; }
-    __host__ __device__ double *dz() const { return (double *)base + 5 * cap; }
-    __host__ __device__ double *t() const { return (double *)base + 6 * cap; }
-    __host__ __device__ uint64_t *rng() const { return (uint64_t *)base + 7 * cap; }
-    __host__ __device__ int32_t *who() const { return (int32_t *)((double *)base + 8 * cap); }  // best hit shape (-1: miss)
-    __host__ __device__ uint32_t *meta() const { return (uint32_t *)((double *)base + 8 * cap) + cap; }  // depth | stack count << 8
-    __host__ __device__ uint32_t *sid() const { return (uint32_t *)((double *)base + 8 * cap) + 2 * cap; }  // slot id of the path
+    static constexpr uint32_t BLK = 64, BLK_BYTES = (uint32_t)BYTES * BLK;
+    enum F8 : int { OX, OY, OZ, DX, DY, DZ, T, RNG };
+    enum F4 : int { WHO, META, SID };
+    // the 8-byte fields of position k: d8(k)[f * 64]; the 4-byte ones: d4(k)[f * 64]
+    __host__ __device__ double *d8(uint32_t k) const {
+        return (double *)(base + (size_t)(k / BLK) * BLK_BYTES) + (k % BLK);
+    }
+    __host__ __device__ uint32_t *d4(uint32_t k) const {
+        return (uint32_t *)(base + (size_t)(k / BLK) * BLK_BYTES + 8 * 8 * BLK) + (k % BLK);
+    }
+    __host__ __device__ double &t(uint32_t k) const { return d8(k)[T * BLK]; }  // best hit t
+    __host__ __device__ int32_t &who(uint32_t k) const { return *(int32_t *)&d4(k)[WHO * BLK]; }  // best hit shape (-1: miss)
 };
 
 // Device view of the workspace for one chunk.
@@ -98,6 +105,31 @@ struct WfView {
     uint32_t s0, ns;  // sample range of the chunk
     uint32_t tile0;   // first tile of the group (index in this rank's tile list)
 };
+
+// What a launch of the wavefront kernels reads besides its iteration: the
+// scene, the frame and the chunk's view (for one parity of the iteration: the
+// two state sets swap roles every bounce).  A frame's blocks, one per (chunk,
+// parity), are written to device memory with one copy before its first
+// launch, and each kernel takes a pointer to its block (16 bytes of kernel
+// arguments instead of 704 by value).  The kernels read the block through
+// kargs(): a scalar pointer the compiler cannot see through, taken again at
+// the top of every trip of their loops, so each field is a scalar load next to
+// its use rather than a value held in an SGPR for the whole kernel (by value,
+// the loop-invariant arguments and their derived addresses spilled 60-70
+// SGPRs of the bounce builds to VGPR lanes, round 5).
+struct WfArgs {
+    dev::Scene sc;
+    FrameParams P;
+    WfView v;
+};
+
+template <class T>
+__device__ __forceinline__ const T &kargs(const T *p) {
+    typedef const __attribute__((address_space(4))) T *cptr;
+    cptr q = (cptr)p;
+    asm volatile("" : "+s"(q));
+    return *(const T *)q;
+}
 
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -190,17 +222,34 @@ __device__ __forceinline__ T ld_path(const T *p) {
 }
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
                                            int who, uint64_t rng, uint32_t meta) {
-    st_path(S.ox() + k, ray.o.x);
-    st_path(S.oy() + k, ray.o.y);
-    st_path(S.oz() + k, ray.o.z);
-    st_path(S.dx() + k, ray.d.x);
-    st_path(S.dy() + k, ray.d.y);
-    st_path(S.dz() + k, ray.d.z);
-    st_path(S.t() + k, best);
-    st_path(S.who() + k, (int32_t)who);
-    st_path(S.rng() + k, (uint64_t)rng);
-    st_path(S.meta() + k, meta);
-    st_path(S.sid() + k, id);
+    double *a = S.d8(k);
+    uint32_t *b = S.d4(k);
+    constexpr uint32_t B = PathSoA::BLK;
+    st_path(a + PathSoA::OX * B, ray.o.x);
+    st_path(a + PathSoA::OY * B, ray.o.y);
+    st_path(a + PathSoA::OZ * B, ray.o.z);
+    st_path(a + PathSoA::DX * B, ray.d.x);
+    st_path(a + PathSoA::DY * B, ray.d.y);
+    st_path(a + PathSoA::DZ * B, ray.d.z);
+    st_path(a + PathSoA::T * B, best);
+    st_path(b + PathSoA::WHO * B, (uint32_t)who);
+    st_path((uint64_t *)a + PathSoA::RNG * B, (uint64_t)rng);
+    st_path(b + PathSoA::META * B, meta);
+    st_path(b + PathSoA::SID * B, id);
+}
+// The state of position p: slot id, ray, rng, meta, pending hit (who, t).
+__device__ __forceinline__ void load_path(const PathSoA &S, uint32_t p, uint32_t *id, Ray *ray, uint64_t *rng,
+                                          uint32_t *meta, int *who, double *best) {
+    const double *a = S.d8(p);
+    const uint32_t *b = S.d4(p);
+    constexpr uint32_t B = PathSoA::BLK;
+    *id = ld_path(b + PathSoA::SID * B);
+    ray->o = dev::v3(ld_path(a + PathSoA::OX * B), ld_path(a + PathSoA::OY * B), ld_path(a + PathSoA::OZ * B));
+    ray->d = dev::v3(ld_path(a + PathSoA::DX * B), ld_path(a + PathSoA::DY * B), ld_path(a + PathSoA::DZ * B));
+    *rng = ld_path((const uint64_t *)a + PathSoA::RNG * B);
+    *meta = ld_path(b + PathSoA::META * B);
+    *who = (int)ld_path(b + PathSoA::WHO * B);
+    *best = ld_path(a + PathSoA::T * B);
 }
 
 // Pixel of a path slot: slot = (s_local * tiles + ti_local) * 256 + thread-in-tile,
@@ -223,6 +272,10 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
 constexpr int WF_PREDICT = 4;
 
+#ifndef PT_WAVE_COMPACT
+#define PT_WAVE_COMPACT 1  // bounce outputs compacted per wave (survivors first): 1 on, 0 every input position stored
+#endif
+
 #ifndef PT_WF_BOUNCE_WAVES
 #define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
 #endif
@@ -234,10 +287,17 @@ constexpr int WF_PREDICT = 4;
 // stores; summed into diag[36..42].
 template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false,
           bool BIGBVH = false>
-__global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FrameParams P, WfView v, int it,
+__global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict__ A, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
-    const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
+    uint32_t count;
+    {
+        const WfArgs &a = kargs(A);
+        const WfView &v = a.v;
+        count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
+        // a progressive frame's chunk stopped by stop_gate: this launch must find no work
+        if (a.P.stop && blockIdx.x == 0 && threadIdx.x == 0 && v.cnt[3]) dev::note_stop(a.sc.guard, count > 0);
+    }
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
     PT_LP_BEGIN();
@@ -250,6 +310,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
     }
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {
         if (DIAG) tst = __builtin_amdgcn_s_memtime();
+        const WfArgs &a = kargs(A);
+        const dev::Scene &sc = a.sc;
+        const FrameParams &P = a.P;
+        const WfView &v = a.v;
         const uint32_t i = base + threadIdx.x;
         bool live = i < count;
         uint32_t id = 0;
@@ -277,14 +341,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
             } else {
                 const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
-                PathSoA S = v.in;
-                id = ld_path(S.sid() + p);
-                ray.o = dev::v3(ld_path(S.ox() + p), ld_path(S.oy() + p), ld_path(S.oz() + p));
-                ray.d = dev::v3(ld_path(S.dx() + p), ld_path(S.dy() + p), ld_path(S.dz() + p));
-                rng.s = ld_path(S.rng() + p);
-                const uint32_t meta = ld_path(S.meta() + p);
-                who = ld_path(S.who() + p);
-                best = ld_path(S.t() + p);
+                uint32_t meta;
+                load_path(v.in, p, &id, &ray, &rng.s, &meta, &who, &best);
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
@@ -297,6 +355,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
         // starts before its best hit.  (Up to 2-3 bounces per launch for paths
         // needing no march measured +0.8 % / -2.5 %, round 2.)
         bool need_march = false, long_job = false;
+        V3 jo_o = dev::v3(0.0, 0.0, 0.0), jo_d = jo_o;  // a march job: the object-space ray and bound interval
+        double jo_st = 0.0, jo_en = 0.0;
         if (live) {
             PT_LP(LIVE);
             if (!FIRST) {
@@ -332,34 +392,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
                 PT_LP(PRE_SLAB);
                 const DShape S = dev::uniform_shape(&sc.shapes[s]);
-                const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
-                double st, en;
-                need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
-                if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
-                    PT_LP(PRE_JOB);
-                    // the 64 B record in four 16-byte non-temporal stores (as eight 8-byte ones: the
-                    // same time; structure of arrays: slower, round 3 jo2)
-                    typedef double d2v __attribute__((ext_vector_type(2)));
-                    d2v *j = (d2v *)(v.jo + (size_t)i * 4);
-                    __builtin_nontemporal_store((d2v){o.x, o.y}, j + 0);
-                    __builtin_nontemporal_store((d2v){o.z, d.x}, j + 1);
-                    __builtin_nontemporal_store((d2v){d.y, d.z}, j + 2);
-                    __builtin_nontemporal_store((d2v){st, en}, j + 3);
-                    // queue order only: a march that will cross the surface (a hit: ~3x
-                    // the iterations of a miss) is predicted by the sign of f at the bound
-                    // entry and at WF_PREDICT points along the chord (inside is f < 0;
-                    // measured on captured cornell jobs: every predicted job a hit, 0.2 %
-                    // of the others)
-                    long_job = march::shape_f_k<FK>(dev::shape_params(S), o.x + d.x * st, o.y + d.y * st,
-                                                    o.z + d.z * st) < 0.0;
-                    const double dt = (en - st) * (1.0 / WF_PREDICT);
-#pragma unroll
-                    for (int q = 0; q < WF_PREDICT; q++) {
-                        const double tq = st + dt * (q + 0.5);
-                        long_job = long_job || march::shape_f_k<FK>(dev::shape_params(S), o.x + d.x * tq,
-                                                                    o.y + d.y * tq, o.z + d.z * tq) < 0.0;
-                    }
-                }
+                jo_o = dev::xf_point(S.inv, ray.o);
+                jo_d = dev::xf_vector(S.inv, ray.d);
+                need_march = march::shape_bound_k<FK>(dev::shape_params(S), jo_o.x, jo_o.y, jo_o.z, jo_d.x, jo_d.y,
+                                                      jo_d.z, &jo_st, &jo_en);
             }
             PT_BSTAMP(5)
             if (any && !need_march) {
@@ -371,13 +407,49 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
                 live = false;
             }
         }
-        // every input position's state is written (ended paths too: whole lines; storeab)
-        if (i < count) PT_LP(STORE);
-        if (i < count)
-        {
-            store_path(v.out, i, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+#if PT_WAVE_COMPACT
+        // The wave's surviving paths (live, or waiting for a march) go to consecutive output positions from the
+        // wave's first one, in input (= id) order, and the positions after them get status 0: the ended paths'
+        // state is not written, and the next bounce gathers from runs with holes only at wave ends (round 5).
+        const uint32_t wbase = base + (threadIdx.x & ~63u);
+        const uint64_t keep = __ballot(live);
+        const uint32_t k = wbase + (uint32_t)__popcll(keep & ((1ull << (threadIdx.x & 63)) - 1ull));
+        if (i < count && (threadIdx.x & 63) >= (uint32_t)__popcll(keep)) v.status[i] = 0u;
+#else
+        const uint32_t k = i;  // every input position's state is written (ended paths too: whole lines; storeab)
+#endif
+        if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
+            PT_LP(PRE_JOB);
+            // the 64 B record in four 16-byte non-temporal stores (as eight 8-byte ones: the
+            // same time; structure of arrays: slower, round 3 jo2)
+            typedef double d2v __attribute__((ext_vector_type(2)));
+            d2v *j = (d2v *)(v.jo + (size_t)k * 4);
+            __builtin_nontemporal_store((d2v){jo_o.x, jo_o.y}, j + 0);
+            __builtin_nontemporal_store((d2v){jo_o.z, jo_d.x}, j + 1);
+            __builtin_nontemporal_store((d2v){jo_d.y, jo_d.z}, j + 2);
+            __builtin_nontemporal_store((d2v){jo_st, jo_en}, j + 3);
+            // queue order only: a march that will cross the surface (a hit: ~3x
+            // the iterations of a miss) is predicted by the sign of f at the bound
+            // entry and at WF_PREDICT points along the chord (inside is f < 0;
+            // measured on captured cornell jobs: every predicted job a hit, 0.2 %
+            // of the others)
+            const march::FParams F = dev::shape_params(dev::uniform_shape(&sc.shapes[dev::uniform_index(
+                dev::uniform_load(&sc.march[0]))]));
+            const V3 o = jo_o, d = jo_d;
+            const double st = jo_st, en = jo_en;
+            long_job = march::shape_f_k<FK>(F, o.x + d.x * st, o.y + d.y * st, o.z + d.z * st) < 0.0;
+            const double dt = (en - st) * (1.0 / WF_PREDICT);
+#pragma unroll
+            for (int q = 0; q < WF_PREDICT; q++) {
+                const double tq = st + dt * (q + 0.5);
+                long_job = long_job || march::shape_f_k<FK>(F, o.x + d.x * tq, o.y + d.y * tq, o.z + d.z * tq) < 0.0;
+            }
         }
-        if (i < count) v.status[i] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
+        if (i < count) PT_LP(STORE);
+        if (i < count && (!PT_WAVE_COMPACT || live)) {
+            store_path(v.out, k, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+            v.status[k] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
+        }
         PT_BSTAMP(6)
     }
 #undef PT_BSTAMP
@@ -399,10 +471,13 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(dev::Scene sc, FramePara
 // bit for bit; only paths that never meet a march skip the per-bounce state
 // round trip through HBM and the per-bounce launch.
 template <bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false>
-__global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParams P, WfView v, int it,
-                                                       uint32_t slice) {
+__global__ __launch_bounds__(256, WAVES) void wf_trace(const WfArgs *__restrict__ A, int it, uint32_t slice) {
     __shared__ uint32_t head;
-    const uint32_t count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
+    uint32_t count;
+    {
+        const WfView &v = kargs(A).v;
+        count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
+    }
     const uint32_t G = gridDim.x;
     const uint32_t runs = (count + slice - 1) / slice;
     const uint32_t per = (runs > blockIdx.x ? (runs - blockIdx.x + G - 1) / G : 0u) * slice;
@@ -416,10 +491,15 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
     Ray ray;
     ray.o = ray.d = dev::v3(0.0, 0.0, 0.0);
     dev::Rng rng{0};
-    MemStack stk{v.ids, (size_t)v.cap, 0, nullptr};
+    MemStack stk{nullptr, 0, 0, nullptr};
     double best = 0.0;
     int who = -1;
     while (have) {
+        const WfArgs &a = kargs(A);
+        const dev::Scene &sc = a.sc;
+        const FrameParams &P = a.P;
+        const WfView &v = a.v;
+        stk.stride = v.cap;
         bool done = false, shade_now = true;
         if (fresh) {
             fresh = false;
@@ -442,18 +522,12 @@ __global__ __launch_bounds__(256, WAVES) void wf_trace(dev::Scene sc, FrameParam
                 }
             } else {
                 const uint32_t p = v.list[k];
-                const PathSoA &S = v.in;
-                id = S.sid()[p];
-                ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
-                ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
-                rng.s = S.rng()[p];
-                const uint32_t meta = S.meta()[p];
+                uint32_t meta;
+                load_path(v.in, p, &id, &ray, &rng.s, &meta, &who, &best);
                 depth = meta & 0xffu;
                 stk.base = v.ids + id;
                 stk.n = (int)(meta >> 8);
                 if (EXT) stk.vb = v.att + id;
-                who = S.who()[p];
-                best = S.t()[p];
             }
         }
         if (!done && shade_now) {
@@ -732,23 +806,26 @@ struct MarchJob {
 };
 
 __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob *j) {
+    const double *a = S.d8(p);
+    constexpr uint32_t B = PathSoA::BLK;
     j->id = p;
-    j->ray.o = dev::v3(S.ox()[p], S.oy()[p], S.oz()[p]);
-    j->ray.d = dev::v3(S.dx()[p], S.dy()[p], S.dz()[p]);
-    j->best = S.t()[p];
-    j->who = S.who()[p];
+    j->ray.o = dev::v3(a[PathSoA::OX * B], a[PathSoA::OY * B], a[PathSoA::OZ * B]);
+    j->ray.d = dev::v3(a[PathSoA::DX * B], a[PathSoA::DY * B], a[PathSoA::DZ * B]);
+    j->best = S.t(p);
+    j->who = S.who(p);
 }
 
 // DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
 // 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
 template <bool DIAG, int FK = march::F_ANY>
-__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc, WfView v, int it, unsigned long long *diag,
-                                                                            uint32_t slice) {
+__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs *__restrict__ A, int it,
+                                                                   unsigned long long *diag, uint32_t slice) {
     __shared__ uint32_t head;
-    const int nm = sc.nmarch;
-    const uint32_t count = v.cnt[it * 4 + 1];
-    const uint32_t *mq = v.mq;
+    const WfArgs &a0 = kargs(A);
+    const int nm = a0.sc.nmarch;
+    const uint32_t count = a0.v.cnt[it * 4 + 1];
+    if (a0.P.stop && blockIdx.x == 0 && threadIdx.x == 0 && a0.v.cnt[3]) dev::note_stop(a0.sc.guard, count > 0);
     // The block's jobs: local index q = 0, 1, ... maps to the queue position
     // pos(q).  slice == 0: one contiguous slice of the queue per block.
     // slice > 0: runs of `slice` consecutive jobs dealt round-robin to the
@@ -776,13 +853,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     bool have = q < per && pos(q) < count;
     // one marched shape and jobs pre-selected by the bounce kernel: a job is
     // its march alone (no select, no ray transform, no bound quadratic here)
-    const bool pre = v.jo != nullptr;
+    const bool pre = a0.v.jo != nullptr;
     int s0 = 0, passes0 = 0;
     double step0 = 0.0;
     march::FParams F0{};
     if (pre) {
-        s0 = dev::uniform_load(&sc.march[0]);
-        const DShape S = dev::uniform_shape(&sc.shapes[s0]);
+        s0 = dev::uniform_load(&a0.sc.march[0]);
+        const DShape S = dev::uniform_shape(&a0.sc.shapes[s0]);
         F0 = dev::shape_params(S);
         step0 = S.p[0];
         passes0 = S.depth;
@@ -791,12 +868,12 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
     march::MarchState ms;
     bool marching = false;
     int km = 0, mshape = -1;
-    auto start_job = [&](uint32_t k) {  // k: queue position
-        const uint32_t id = mq[k];  // position in the bounce's output
+    auto start_job = [&](const WfView &v, uint32_t k) {  // k: queue position
+        const uint32_t id = v.mq[k];  // position in the bounce's output
         if (pre) {
             cur.id = id;
-            cur.best = v.out.t()[id];
-            cur.who = v.out.who()[id];
+            cur.best = v.out.t(id);
+            cur.who = v.out.who(id);
             const double2 *j = v.jo + (size_t)id * 4;
             const double2 a = j[0], b = j[1], c = j[2], e = j[3];
             march::march_start<FK>(F0, step0, passes0, a.x, a.y, b.x, b.y, c.x, c.y, e.x, e.y, &ms);
@@ -807,7 +884,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
         }
     };
     PT_MREG_KERNEL_BEGIN();
-    if (have) start_job(pos(q));
+    if (have) start_job(a0.v, pos(q));
     V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
     unsigned long long dtrips[16], dcyc[16], dlanes[4];
@@ -844,7 +921,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 const int st = march::march_step<false, true, FK>(ms, &mst);
                 PT_MREG_STEP_END();
                 if (st != march::M_RUNNING) {
-                    if (st == march::M_GUARD) dev::note_guard(sc.guard);
+                    if (st == march::M_GUARD) dev::note_guard(kargs(A).sc.guard);
                     // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
                     if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > cur.best) &&
                         (ms.t < cur.best || mshape > cur.who)) {
@@ -856,6 +933,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 }
             } else {
                 // select: next marched shape whose bound is entered before `best`
+                const dev::Scene &sc = kargs(A).sc;
                 while (km < nm) {
                     const int s = sc.march[km++];
                     const DBox &b = sc.boxes[s];
@@ -880,11 +958,12 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
                 const uint32_t fid = cur.id;
                 const double fbest = cur.best;
                 const int fwho = cur.who;
+                const WfView &v = kargs(A).v;
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
-                if (have) start_job(pos(q));
-                v.out.t()[fid] = fbest;
-                v.out.who()[fid] = fwho;
+                if (have) start_job(v, pos(q));
+                v.out.t(fid) = fbest;
+                v.out.who(fid) = fwho;
                 if (have && !pre) {
                     inv = dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
                     km = 0;
@@ -916,10 +995,18 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(dev::Scene sc
 // sample: a version unwinding 8 samples level by level together needs more
 // registers and measured slower (the kernel is latency-bound: occupancy wins).
 template <bool EXT>
-__global__ __launch_bounds__(256) void wf_reduce(dev::Scene sc, FrameParams P, WfView v, int first, int last,
+__global__ __launch_bounds__(256) void wf_reduce(const WfArgs *__restrict__ A, int first, int last,
                                                  double *__restrict__ out) {
+    const WfArgs &args = kargs(A);
+    const dev::Scene &sc = args.sc;
+    const FrameParams &P = args.P;
+    const WfView &v = args.v;
     const uint32_t pl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pl >= v.npix || v.cnt[3]) return;  // v.cnt[3]: a stopped frame's chunk, nothing to sum
+    if (v.cnt[3]) {  // a stopped frame's chunk: nothing to sum
+        if (P.stop && pl == 0) dev::note_stop(sc.guard, false);
+        return;
+    }
+    if (pl >= v.npix) return;
     uint32_t x, y, sl, pl2;
     slot_pixel(P, v, pl, &x, &y, &sl, &pl2);
     const uint32_t ti = v.tile0 + pl / (TILE * TILE), th = pl % (TILE * TILE);
@@ -1006,6 +1093,7 @@ hipError_t timer_collect(KernelTimer *t, double *ms, uint32_t *launches) {
 }
 
 // ------------------------------------------------------------- host driver
+static void free_args(WaveWorkspace *ws);
 void wave_workspace_free(WaveWorkspace *ws) {
     for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
         if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
@@ -1013,12 +1101,14 @@ void wave_workspace_free(WaveWorkspace *ws) {
         ws->side[k] = nullptr;
         ws->join[k] = nullptr;
     }
+    free_args(ws);
     if (ws->fork) (void)hipEventDestroy(ws->fork);
     if (ws->reduced) (void)hipEventDestroy(ws->reduced);
     if (ws->done) (void)hipEventDestroy(ws->done);
     if (ws->bev) (void)hipEventDestroy(ws->bev);
     if (ws->mev) (void)hipEventDestroy(ws->mev);
-    ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = nullptr;
+    if (ws->args_ev) (void)hipEventDestroy(ws->args_ev);
+    ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = ws->args_ev = nullptr;
     ws->used = false;
     timer_free(ws->timer);
     ws->timer = nullptr;
@@ -1027,6 +1117,41 @@ void wave_workspace_free(WaveWorkspace *ws) {
     if (ws->base) (void)hipFree(ws->base);
     ws->base = nullptr;
     ws->bytes = 0;
+}
+
+// The launches' argument blocks: a pinned host staging buffer and its device copy (render_wave_nw).
+static void free_args(WaveWorkspace *ws) {
+    if (ws->args_pending && ws->args_ev) (void)hipEventSynchronize(ws->args_ev);
+    if (ws->args_host) (void)hipHostFree(ws->args_host);
+    if (ws->args_dev) (void)hipFree(ws->args_dev);
+    ws->args_host = ws->args_dev = nullptr;
+    ws->args_bytes = 0;
+    ws->args_pending = false;
+}
+
+static hipError_t reserve_args(WaveWorkspace *ws, size_t bytes) {
+    hipError_t e;
+    // the staging buffer is free again once the previous frame's copy has run
+    if (ws->args_pending) {
+        if ((e = hipEventSynchronize(ws->args_ev)) != hipSuccess) return e;
+        ws->args_pending = false;
+    }
+    if (bytes <= ws->args_bytes) return hipSuccess;
+    // growing: the previous frame's kernels must be done with the device blocks
+    if (ws->used && (e = hipEventSynchronize(ws->done)) != hipSuccess) return e;
+    free_args(ws);
+    if (bytes < ((size_t)64 << 10)) bytes = (size_t)64 << 10;
+    if ((e = hipHostMalloc(&ws->args_host, bytes, hipHostMallocDefault)) != hipSuccess) {
+        ws->args_host = nullptr;
+        return e;
+    }
+    if ((e = hipMalloc(&ws->args_dev, bytes)) != hipSuccess) {
+        ws->args_dev = nullptr;
+        free_args(ws);
+        return e;
+    }
+    ws->args_bytes = bytes;
+    return hipSuccess;
 }
 
 static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
@@ -1052,35 +1177,35 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
 // BVH nodes per octant layout from which the bounce runs its FMA_SLAB build
 // (dev::closest_nomarch): C5's 100k-sphere tree has ~200k, cornell's ~960.
 template <int NW, bool FIRST>
-static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const FrameParams &P,
-                          const WfView &v, int it, unsigned long long *diag, int fkind, int waves) {
+static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it,
+                          unsigned long long *diag, int fkind, int waves) {
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
-        wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (fkind != march::F_HEART) {  // another ray-marched function: the generic build
-        wf_bounce<NW, FIRST, 2, false, march::F_ANY><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        wf_bounce<NW, FIRST, 2, false, march::F_ANY><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (diag) {
-        wf_bounce<NW, FIRST, 2, true, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it, diag);
+        wf_bounce<NW, FIRST, 2, true, march::F_HEART><<<blocks, 256, 0, st>>>(A, it, diag);
         return;
     }
     if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
-        wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH (C5): the FMA slab build
-        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(sc, P, v, it);
+        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves
-    case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    case 5: wf_bounce<NW, FIRST, 5, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    case 6: wf_bounce<NW, FIRST, 6, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    case 8: wf_bounce<NW, FIRST, 8, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
-    default: wf_bounce<NW, FIRST, 3, false, march::F_HEART><<<blocks, 256, 0, st>>>(sc, P, v, it); break;
+    case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 5: wf_bounce<NW, FIRST, 5, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 6: wf_bounce<NW, FIRST, 6, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 8: wf_bounce<NW, FIRST, 8, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    default: wf_bounce<NW, FIRST, 3, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
     }
 }
 
@@ -1103,17 +1228,16 @@ static uint32_t resident_blocks(K kern) {
 // chunk's marches — so per-bounce launches are the default.  The diag build
 // always runs wf_bounce.
 template <bool FIRST>
-static void launch_trace(hipStream_t st, const dev::Scene &sc, const FrameParams &P, const WfView &v, int it,
-                         int fkind, uint32_t slice) {
+static void launch_trace(hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it, int fkind, uint32_t slice) {
     if (sc.ext) {
         static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY, true>);
-        wf_trace<FIRST, 2, march::F_ANY, true><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+        wf_trace<FIRST, 2, march::F_ANY, true><<<nb, 256, 0, st>>>(A, it, slice);
     } else if (fkind != march::F_HEART) {
         static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY>);
-        wf_trace<FIRST, 2, march::F_ANY><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+        wf_trace<FIRST, 2, march::F_ANY><<<nb, 256, 0, st>>>(A, it, slice);
     } else {
         static const uint32_t nb = resident_blocks(wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART>);
-        wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART><<<nb, 256, 0, st>>>(sc, P, v, it, slice);
+        wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART><<<nb, 256, 0, st>>>(A, it, slice);
     }
 }
 
@@ -1128,6 +1252,9 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     if (ws->device != dev || ws->side_priority != ws->tune.wf_side_priority) {  // streams and events belong to one device
         // the previous frame must be done with the streams and the workspace
         if (ws->used && ws->done && (e = hipEventSynchronize(ws->done)) != hipSuccess) return e;
+        free_args(ws);  // (the device blocks live on the old device)
+        if (ws->args_ev) (void)hipEventDestroy(ws->args_ev);
+        ws->args_ev = nullptr;
         for (int k = 0; k < WaveWorkspace::MAX_SLOTS - 1; k++) {
             if (ws->side[k]) (void)hipStreamDestroy(ws->side[k]);
             if (ws->join[k]) (void)hipEventDestroy(ws->join[k]);
@@ -1149,6 +1276,7 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->bev && (e = hipEventCreateWithFlags(&ws->bev, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->mev && (e = hipEventCreateWithFlags(&ws->mev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ws->args_ev && (e = hipEventCreateWithFlags(&ws->args_ev, hipEventDisableTiming)) != hipSuccess) return e;
     for (int k = 0; k < slots - 1; k++) {
         if (!ws->side[k]) {
             int lo = 0, hi = 0;  // least and greatest priority (greatest is numerically lowest)
@@ -1268,12 +1396,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         if (want < march_blocks) march_blocks = want;
     }
     const uint32_t march_slice = (uint32_t)tu.wf_march_slice;
-    // the side streams start after everything the caller queued on st
-    if (slots > 1) {
-        if ((e = hipEventRecord(ws->fork, st)) != hipSuccess) return e;
-        for (int k = 0; k < slots - 1; k++)
-            if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
-    }
     const bool fused = tu.wf_fused && !ws->diag;
     // Chunks run in rounds of `slots`, chunk j of a round on stream j, and are
     // enqueued iteration by iteration across the round.  With wf_pingpong the
@@ -1300,46 +1422,68 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             s0 += n;
         }
     }
+    // The launches' argument blocks (WfArgs): chunk ci (on slot ci % slots) at iteration parity h is block
+    // 2 ci + h.  They are written to the pinned staging buffer, which the previous frame's copy must have read,
+    // and copied to the device on st after the previous frame's kernels (the wait on ws->done above), before
+    // the side streams fork.
+    const size_t nargs = chunk_list.size() * 2;
+    if ((e = reserve_args(ws, nargs * sizeof(WfArgs))) != hipSuccess) return e;
+    WfArgs *ah = (WfArgs *)ws->args_host, *ad = (WfArgs *)ws->args_dev;
+    for (size_t ci = 0; ci < chunk_list.size(); ci++) {
+        const Chunk &ch = chunk_list[ci];
+        const int j = (int)(ci % (size_t)slots);
+        WfView v = sl[j].v;
+        v.tile0 = P0.tile_begin + ch.g0;
+        v.npix = ch.gt * TILE * TILE;
+        v.s0 = ch.s0;
+        v.ns = ch.ns;
+        for (int h = 0; h < 2; h++) {
+            v.in = sl[j].set[h];
+            v.out = sl[j].set[h ^ 1];
+            ah[2 * ci + h] = WfArgs{sc, P0, v};
+        }
+    }
+    if ((e = hipMemcpyAsync(ad, ah, nargs * sizeof(WfArgs), hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ws->args_ev, st)) != hipSuccess) return e;
+    ws->args_pending = true;
+    // the side streams start after everything the caller queued on st
+    if (slots > 1) {
+        if ((e = hipEventRecord(ws->fork, st)) != hipSuccess) return e;
+        for (int k = 0; k < slots - 1; k++)
+            if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
+    }
     // wf_pingpong bit 0: chain the bounce launches; bit 1: chain the march launches
     const bool pingpong = (tu.wf_pingpong & 1) && slots > 1, mchain = (tu.wf_pingpong & 2) && slots > 1;
     bool chained = false, mchained = false;  // ws->bev / ws->mev hold a launch to wait for
     for (size_t r0 = 0; r0 < chunk_list.size(); r0 += (size_t)slots) {
         const int nr = (int)(chunk_list.size() - r0 < (size_t)slots ? chunk_list.size() - r0 : (size_t)slots);
-        for (int j = 0; j < nr; j++) {  // the round's chunks: views and cleared counters
-            const Chunk &ch = chunk_list[r0 + j];
+        for (int j = 0; j < nr; j++) {  // the round's chunks: cleared counters
             const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
-            WfView &v = sl[j].v;
-            v.tile0 = P0.tile_begin + ch.g0;
-            v.npix = ch.gt * TILE * TILE;
-            v.s0 = ch.s0;
-            v.ns = ch.ns;
-            const uint32_t paths = v.ns * v.npix;
-            (void)paths;  // (every bounce writes the status of each of its inputs; compaction reads no further)
-            if ((e = hipMemsetAsync(v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(sl[j].v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
             if (P0.stop) {
-                stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, -1);
+                stop_gate<<<1, 64, 0, cs>>>(P0.stop, sl[j].v.cnt, -1);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
         }
         for (int it = 0; it < iters; it++) {
             for (int j = 0; j < nr; j++) {
                 const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
-                WfView &v = sl[j].v;
+                const Chunk &ch = chunk_list[r0 + j];
+                const WfArgs *A = ad + 2 * (r0 + j) + (it & 1);
+                const WfView &v = sl[j].v;
                 uint32_t *cp_blk = sl[j].cp_blk;
-                const uint32_t paths = v.ns * v.npix;
-                v.in = sl[j].set[it & 1];
-                v.out = sl[j].set[(it + 1) & 1];
+                const uint32_t paths = ch.ns * ch.gt * TILE * TILE;
                 uint32_t bb = (paths + 255) / 256;
                 if (bb > WF_BOUNCE_CAP) bb = WF_BOUNCE_CAP;
                 if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
                 if (it == 0) {
-                    if (fused) launch_trace<true>(cs, sc, P0, v, 0, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, P0, v, 0, ws->diag, fkind, tu.wf_bounce_waves);
+                    if (fused) launch_trace<true>(cs, sc, A, 0, fkind, (uint32_t)tu.wf_trace_slice);
+                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves);
                 } else {
-                    if (fused) launch_trace<false>(cs, sc, P0, v, it, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, false>(bb, cs, sc, P0, v, it, ws->diag, fkind, tu.wf_bounce_waves);
+                    if (fused) launch_trace<false>(cs, sc, A, it, fkind, (uint32_t)tu.wf_trace_slice);
+                    else launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves);
                 }
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
@@ -1365,11 +1509,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)
-                    wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
+                    wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
                 else if (ws->diag)
-                    wf_march<true, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, ws->diag, march_slice);
+                    wf_march<true, march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, ws->diag, march_slice);
                 else
-                    wf_march<false, march::F_HEART><<<march_blocks, 256, 0, cs>>>(sc, v, it, nullptr, march_slice);
+                    wf_march<false, march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (mchain) {
@@ -1381,17 +1525,18 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         // the per-pixel sums take the chunks in order
         for (int j = 0; j < nr; j++) {
             const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
-            WfView &v = sl[j].v;
-            const uint32_t s0 = v.s0;
+            const Chunk &ch = chunk_list[r0 + j];
+            const WfArgs *A = ad + 2 * (r0 + j);
+            const uint32_t npix = ch.gt * TILE * TILE;
             if (slots > 1 && r0 + j > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
             // first: 1 = sums from zero, 2 = from out's running sums; last: 1 = means, 2 = running sums to out
-            const int first = s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
-            const int last = s0 + v.ns >= s_end ? (s_end == P0.spp ? 1 : 2) : 0;
+            const int first = ch.s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
+            const int last = ch.s0 + ch.ns >= s_end ? (s_end == P0.spp ? 1 : 2) : 0;
             if (sc.ext)
-                wf_reduce<true><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, first, last, out);
+                wf_reduce<true><<<(npix + 255) / 256, 256, 0, cs>>>(A, first, last, out);
             else
-                wf_reduce<false><<<(v.npix + 255) / 256, 256, 0, cs>>>(sc, P0, v, first, last, out);
+                wf_reduce<false><<<(npix + 255) / 256, 256, 0, cs>>>(A, first, last, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;

@@ -3,15 +3,16 @@
  *
  *   abi_check layout                 sizeof / offsetof of every boundary struct as
  *                                    this compiler lays it out == pt_abi_layout
- *   abi_check legacy <scene.json>    a 0.1.0 / 0.2.0 caller: the 32-byte struct with
- *                                    `reserved` = 0 where struct_size now sits and an
- *                                    image loader set, at the very end of a readable
- *                                    page, the next page PROT_NONE, so a read past it
- *                                    faults; the scene (with an ImageTexture) must load
- *                                    through that loader, never the built-in reader; a
- *                                    16-byte struct (struct_size 16) must load without
- *                                    reading past it; a struct_size below 16 must be
- *                                    refused
+ *   abi_check legacy <scene.json>    old callers, `reserved` = 0 where struct_size now
+ *                                    sits: 0.1.0's 16-byte struct at the very end of a
+ *                                    readable page, the next page PROT_NONE, so a read
+ *                                    past it faults, must load the scene (with an
+ *                                    ImageTexture, through the built-in reader); 0.2.0's
+ *                                    32-byte struct with an image loader set loads it
+ *                                    without calling the loader (0 cannot tell the two
+ *                                    apart: ABI 4); the current struct calls its loader;
+ *                                    a 16-byte struct (struct_size 16) loads without
+ *                                    reading past it; a struct_size below 16 is refused
  *   abi_check render <scene.json> <w> <h> <spp> <depth> <seed> <out.f64>
  *                                    Scene::from_json -> ThreadPoolRenderer::new ->
  *                                    start_rendering -> render_step (blocking) through
@@ -141,24 +142,50 @@ static int do_legacy(const char *path) {
         return 1;
     }
     int calls = 0;
-    opts_v02 *o = (opts_v02 *)(mem + pg - sizeof(opts_v02));  /* the next byte is unreadable */
+    /* 0.1.0: the 16 bytes {random_spheres, reserved = 0, seed} against the page end */
+    uint32_t *o10 = (uint32_t *)(mem + pg - 16);
+    o10[0] = 1;
+    o10[1] = 0;
+    *(uint64_t *)(o10 + 2) = 7;
+    pt_scene *s = NULL;
+    int rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o10, &s);
+    if (rc != PT_OK) {
+        fprintf(stderr, "0.1.0 opts: status %d: %s\n", rc, pt_last_error());
+        return 1;
+    }
+    printf("0.1.0 opts: %d shapes, %d materials\n", pt_scene_num_shapes(s), pt_scene_num_materials(s));
+    pt_scene_destroy(s);
+    /* 0.2.0: the 32-byte struct with a loader and reserved = 0 (ABI 4: the loader is not read) */
+    opts_v02 *o = (opts_v02 *)(mem + pg - sizeof(opts_v02));
     o->random_spheres = 1;
     o->reserved = 0;
     o->seed = 7;
     o->load_image = counting_loader;
     o->image_user = &calls;
-    pt_scene *s = NULL;
-    int rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o, &s);
+    s = NULL;
+    rc = pt_scene_create_from_json(json, len, (const pt_scene_opts *)o, &s);
     if (rc != PT_OK) {
         fprintf(stderr, "0.2.0 opts: status %d: %s\n", rc, pt_last_error());
         return 1;
     }
-    if (calls == 0) {
-        fprintf(stderr, "0.2.0 opts: the caller's image loader was not used\n");
+    if (calls != 0) {
+        fprintf(stderr, "0.2.0 opts (struct_size 0): the loader was read and called\n");
         return 1;
     }
-    printf("0.2.0 opts: %d shapes, %d materials, loader called %d times\n", pt_scene_num_shapes(s),
-           pt_scene_num_materials(s), calls);
+    printf("0.2.0 opts: %d shapes, loader not called\n", pt_scene_num_shapes(s));
+    pt_scene_destroy(s);
+    /* the current struct with its loader: called */
+    pt_scene_opts withl = PT_SCENE_OPTS_INIT;
+    withl.seed = 7;
+    withl.load_image = counting_loader;
+    withl.image_user = &calls;
+    s = NULL;
+    rc = pt_scene_create_from_json(json, len, &withl, &s);
+    if (rc != PT_OK || calls == 0) {
+        fprintf(stderr, "current opts with a loader: status %d, %d loader calls: %s\n", rc, calls, pt_last_error());
+        return 1;
+    }
+    printf("current opts: loader called %d times\n", calls);
     pt_scene_destroy(s);
     /* the 16 bytes {random_spheres, struct_size = 16, seed} against the page end: no loader is read */
     uint32_t *o16 = (uint32_t *)(mem + pg - 16);

@@ -90,7 +90,7 @@ def abi_check_bin():
 
 
 def test_abi_version(pt):
-    assert pt.lib().pt_abi_version() == pt.ABI_VERSION == 3
+    assert pt.lib().pt_abi_version() == pt.ABI_VERSION == 4
 
 
 @pytest.mark.parametrize("which", [0, 1, 2, 3, 4, 5])
@@ -115,10 +115,12 @@ def test_plain_c_caller_layout():
     assert out.stdout.count("match") == 6
 
 
-def test_legacy_opts_keep_their_loader_and_are_not_read_past():
-    """A 0.2.0 caller's 32-byte pt_scene_opts (`reserved` = 0 where struct_size
-    sits now, an image loader set) placed against an unreadable page: the scene
-    (with an ImageTexture) loads through that loader, not the built-in reader;
+def test_legacy_opts_are_not_read_past():
+    """A 0.1.0 caller's 16-byte pt_scene_opts (`reserved` = 0 where struct_size
+    sits now) placed against an unreadable page loads the scene (with an
+    ImageTexture) without touching the page; a 0.2.0 caller's 32-byte struct
+    (struct_size 0, a loader set) loads it without calling the loader (0 cannot
+    tell the two apart, ADVICE r4: ABI 4); the current struct calls its loader;
     a 16-byte struct (struct_size 16) loads without touching the page;
     struct_size 8 is refused (no silent fallback for old callers)."""
     import subprocess
@@ -126,6 +128,7 @@ def test_legacy_opts_keep_their_loader_and_are_not_read_past():
                          cwd=str(ROOT))
     assert out.returncode == 0, (out.returncode, out.stderr)
     assert "struct_size 8 refused" in out.stdout
+    assert "0.1.0 opts" in out.stdout and "loader not called" in out.stdout
     assert "loader called" in out.stdout and "16-byte opts" in out.stdout
 
 

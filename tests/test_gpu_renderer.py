@@ -97,19 +97,25 @@ def test_gui_restart_sequence_and_stop(pt, cornell):
     sampled_rows_check(osc, buf, w, h, 1, np.arange(h), n=4096, seed=1)
     # high-sampling pass: 100 spp, abandoned early by a stop (camera moved)
     r.stop_rendering()
+    pt.render_stop_stats(r)  # clear
     r.start_rendering(cam, pt.ImageParams(w, h), 100, seed=1)
     t0 = time.perf_counter()
     r.stop_rendering()
     t_stop = time.perf_counter() - t0
     with pytest.raises(pt.PtError):
         r.render_step(buf)  # nothing in flight after a stop
-    # the same 100 spp frame to the end, for comparison of the stop time
+    skipped, worked = pt.render_stop_stats(r)
+    # the mechanism, not the clock: every launch that met the stop found nothing to do
+    assert worked == 0, (skipped, worked)
+    # the same 100 spp frame to the end, for comparison of the stop time (logged only)
     r.start_rendering(cam, pt.ImageParams(w, h), 100, seed=1)
     t0 = time.perf_counter()
     while not r.render_step(buf):
         pass
     t_full = time.perf_counter() - t0
-    assert t_stop < 0.5 * t_full, (t_stop, t_full)
+    print("stop right after start: %.1f ms (%d launches skipped); the whole frame: %.1f ms"
+          % (t_stop * 1e3, skipped, t_full * 1e3))
+    assert pt.render_stop_stats(r) == (0, 0)  # a frame run to the end meets no stop
     sampled_rows_check(osc, buf, w, h, 100, np.arange(h), n=1024, seed=2)
 
 
@@ -127,11 +133,13 @@ def test_stop_waits_only_for_running_launches(pt, cornell):
     t0 = time.perf_counter()
     r.stop_rendering()
     t_stop = time.perf_counter() - t0
-    print("stop of a 3840x2160 1024 spp frame after 0.8 s: %.1f ms" % (t_stop * 1e3))
-    # the evidence is the logged time (5-8 ms on an idle box, profiles/r3/stop_probe_c3size.txt); the bound
-    # only has to separate "queued launches skipped" from "queued launches drained": draining the running
-    # band and the queued one takes ~0.5-1 s, so a loaded shared box cannot fail a working stop
-    assert t_stop < 0.4, t_stop
+    skipped, worked = pt.render_stop_stats(r)
+    print("stop of a 3840x2160 1024 spp frame after 0.8 s: %.1f ms; %d queued launches skipped, %d worked"
+          % (t_stop * 1e3, skipped, worked))
+    # the mechanism (the time is logged only: 5-8 ms on an idle box, profiles/r3/stop_probe_c3size.txt): the
+    # launches queued behind the fired gate (the rest of the running band's chunks and the queued band) met the
+    # stop and did nothing, so the call waited only for the kernels already running
+    assert skipped > 0 and worked == 0, (skipped, worked)
     w2, h2 = 320, 180
     buf = np.zeros((w2 * h2, 3))
     r.start_rendering(cam, pt.ImageParams(w2, h2), 4, seed=1)

@@ -146,3 +146,17 @@ def test_cli_render_interrupted_and_resumed(tmp_path):
     assert not ck.exists()
     assert (tmp_path / "one.f64").read_bytes() == (tmp_path / "res.f64").read_bytes()
     assert (tmp_path / "one.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+
+
+def test_cli_refuses_an_unloadable_checkpoint(tmp_path):
+    """An existing checkpoint file that does not load (here: not a checkpoint) stops the CLI with exit 1 and the
+    library's message; the file is left as it was, never overwritten by a frame started from sample 0."""
+    import subprocess
+    exe = str(ROOT / "tools" / "pt_render")
+    ck = tmp_path / "frame.ckpt"
+    ck.write_bytes(b"not a checkpoint at all")
+    r = subprocess.run([exe, str(ROOT / "scenes" / "cornell_box.json"), "4", "32", "16", "-c", str(ck), "-n", "2",
+                        "-o", ""], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1, r.stderr
+    assert "not a checkpoint file" in r.stderr
+    assert ck.read_bytes() == b"not a checkpoint at all"

@@ -280,7 +280,8 @@ int main(int argc, char **argv) {
         while (fread(&j, sizeof j, 1, f) == 1) jobs.push_back(j);
         fclose(f);
         int shown = 0, want = argc > 3 ? atoi(argv[3]) : 10;
-        for (size_t i = 0; i < jobs.size() && shown < want; i++) {
+        const long only = argc > 4 ? atol(argv[4]) : -1;  // one job by index
+        for (size_t i = only >= 0 ? (size_t)only : 0; i < jobs.size() && shown < want; i++) {
             const Job &q = jobs[i];
             march::MarchState m;
             march::MarchStats ms{0, 0, 0, 0};

@@ -15,6 +15,9 @@
 // Exit status: 0 done, 1 error (the library's message on stderr), 2 usage, 3 stopped with a checkpoint.
 #include <hip/hip_runtime_api.h>
 
+#include <sys/stat.h>
+
+#include <cerrno>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -119,7 +122,12 @@ int main(int argc, char **argv) {
         }
         uint32_t done = 0;
         pt_checkpoint c;
-        if (pt_checkpoint_load(ckpt.c_str(), &c, nullptr, 0) == PT_OK) {
+        // start fresh only when there is no checkpoint file; an existing one that does not load (corrupt, not a
+        // checkpoint, unreadable) is an error, never overwritten
+        struct stat sb;
+        const bool exists = ::stat(ckpt.c_str(), &sb) == 0 || errno != ENOENT;
+        if (exists && (rc = pt_checkpoint_load(ckpt.c_str(), &c, nullptr, 0)) != PT_OK) return fail(ckpt.c_str(), rc);
+        if (exists) {
             if (c.width != w || c.height != h || c.samples_number != spp || c.seed != seed || c.depth != depth ||
                 c.scene_key != key || c.world != 1) {
                 std::fprintf(stderr, "pt_render: %s belongs to another frame\n", ckpt.c_str());

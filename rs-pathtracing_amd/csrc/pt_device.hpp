@@ -95,6 +95,9 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 #ifndef PT_SLAB32
 #define PT_SLAB32 1  // the large-tree builds' BVH slab test in f32 with a conservative widening (C5 +1.3 %, r4f)
 #endif
+#ifndef PT_RECT_SIGN
+#define PT_RECT_SIGN 1  // rectangles: rays moving away from the plane rejected before the division (round 5)
+#endif
 #ifndef PT_AXIS_LEAF
 #define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,
                         // 2 in the large-tree (FMA_SLAB) builds only (C5 +3.2 %; in the C2 bounce the extra path
@@ -226,6 +229,10 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         const double *m = s.inv;
         const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
+        // a ray moving away from the plane (oz, dz of one sign, or oz = 0) has t = -oz / dz <= 0, below a
+        // positive min_t: rejected without the division (NaN and dz = 0, the range test's quirk, go on)
+        if (PT_RECT_SIGN && min_t > 0.0 && dz != 0.0 && dz == dz && oz == oz && (oz == 0.0 || (oz < 0.0) == (dz < 0.0)))
+            return false;
         const double tt = -oz / dz;
         if (tt < min_t || tt > max_t) return false;
         PT_LP(RECT_ROWS);

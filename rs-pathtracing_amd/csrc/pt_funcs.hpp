@@ -312,10 +312,14 @@ PT_HD bool shape_bound(const FParams &F, double ox, double oy, double oz, double
 // whose marched shapes are all Hearts runs the Heart-only build: no dispatch,
 // no unused constants in registers); FK = F_ANY dispatches on F.func.
 constexpr int F_ANY = -1;
+// F_NONE: the scene has no ray-marched shape (the bounce build for large BVHs without one, C5): the helpers
+// below are never reached at run time and compile to nothing
+constexpr int F_NONE = -2;
 
 template <int FK>
 PT_HD double shape_f_k(const FParams &F, double x, double y, double z) {
-    if constexpr (FK == F_HEART) return f_heart(x, y, z);
+    if constexpr (FK == F_NONE) return 0.0;
+    else if constexpr (FK == F_HEART) return f_heart(x, y, z);
     else return shape_f(F, x, y, z);
 }
 template <int FK>
@@ -342,7 +346,10 @@ PT_HD DM shape_mag_k(const FParams &F, double xm, double ym, double zm) {
 template <int FK>
 PT_HD bool shape_bound_k(const FParams &F, double ox, double oy, double oz, double dx, double dy, double dz,
                          double *start, double *end) {
-    if constexpr (FK == F_HEART) {
+    if constexpr (FK == F_NONE) {
+        *start = *end = 0.0;
+        return false;
+    } else if constexpr (FK == F_HEART) {
         FParams H{};
         H.func = F_HEART;
         return shape_bound(H, ox, oy, oz, dx, dy, dz, start, end);
@@ -352,7 +359,9 @@ PT_HD bool shape_bound_k(const FParams &F, double ox, double oy, double oz, doub
 }
 template <int FK>
 PT_HD void shape_gradient_k(const FParams &F, double px, double py, double pz, double *n) {
-    if constexpr (FK == F_HEART) {
+    if constexpr (FK == F_NONE) {
+        n[0] = n[1] = n[2] = 0.0;
+    } else if constexpr (FK == F_HEART) {
         FParams H{};
         H.func = F_HEART;
         shape_gradient(H, px, py, pz, n);

@@ -517,7 +517,7 @@ constexpr int FOLD_MAX = 3;     // literal steps an iteration may take when the 
 #define PT_LIT_DOUBLE 1  // literal batches after failed proofs double per failure in a row (0: one step each)
 #endif
 #ifndef PT_MARCH_GRID
-#define PT_MARCH_GRID 1  // proofs along the coordinates' exact grid steps, no drift term for in-binade blocks
+#define PT_MARCH_GRID 0  // proofs along the coordinates' exact grid steps, no drift term for in-binade blocks
 #endif
 constexpr int LIT_BATCH = PT_LIT_DOUBLE ? 2 : 1;  // literal steps after a proof that proved no block
 constexpr int LIT_DOUBLINGS = PT_LIT_DOUBLE ? 5 : 0;

@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
             PT_LP(LIVE);
             if (!FIRST) {
                 V3 leaf;
-                const bool ended = dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
+                const bool ended = dev::shade<false, FK, EXT>(kargs(A).sc, who, best, ray, depth, stk, rng, P.s11, &leaf);
                 PT_BSTAMP(2)
                 if (ended) {
                     // the leaf radiance and the stack depth; wf_reduce unwinds
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
             // miss matters (any hit gives black), so a path with a hit found
             // needs no march either
             const bool any = depth == 0;
-            dev::closest_nomarch<false, EXT, BIGBVH>(sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+            dev::closest_nomarch<false, EXT, BIGBVH>(kargs(A).sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             PT_BSTAMP(4)
             // does any marched shape's bound start before the best hit? (the
             // march kernel marches it)
@@ -1196,7 +1196,10 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
         return;
     }
     if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH (C5): the FMA slab build
-        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
+        if (sc.nmarch == 0)  // (C5) no marched shape: no march pre-check or Heart code in the build
+            wf_bounce<NW, FIRST, 3, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it);
+        else
+            wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves

@@ -43,6 +43,8 @@ int hip_fail(hipError_t e, const char *what) {
 
 uint32_t tiles_x_of(uint32_t w) { return (w + TILE - 1) / TILE; }
 uint32_t tiles_y_of(uint32_t h) { return (h + TILE - 1) / TILE; }
+// the smallest band of a progressive frame, in samples (enough paths to fill the device)
+constexpr uint64_t BAND_MIN_SAMPLES = (uint64_t)1 << 24;
 
 }  // namespace
 
@@ -779,10 +781,15 @@ int pt_render_start(pt_renderer *r, const pt_camera *cam, uint32_t w, uint32_t h
     if (int rc = frame_prologue(r, w, h)) return rc;
     r->frame = frame_params(r, *cam, w, h, spp, seed);
     r->frame.stop = r->d_stop;
-    // ~8 bands of whole tile rows: a band is one pass of the engine over
-    // 1/8 of the frame, big enough to fill the device
+    // ~8 bands of whole tile rows, each a pass of the engine over 1/8 of the frame, but no band under
+    // BAND_MIN_SAMPLES: a band of the reference GUI's 1-spp preview at 1600x900 (main.rs:264) would otherwise be
+    // 160k samples, a chain of ~260 launches that each find a few paths (a 78 ms frame, round 5).  The stop
+    // latency does not depend on the band size (stop_gate runs at every chunk start and compaction).
     const uint32_t ty = tiles_y_of(h);
-    const uint32_t band = ty >= 8 ? ty / 8 : 1;
+    const uint64_t row_samples = (uint64_t)tiles_x_of(w) * TILE * TILE * spp;
+    const uint32_t min_rows = (uint32_t)((BAND_MIN_SAMPLES + row_samples - 1) / row_samples);
+    uint32_t band = ty >= 8 ? ty / 8 : 1;
+    if (band < min_rows) band = min_rows < ty ? min_rows : ty;
     release_bands(r);
     for (uint32_t t0 = 0; t0 < ty; t0 += band) {
         pt_renderer::Band b;

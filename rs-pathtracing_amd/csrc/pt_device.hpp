@@ -96,7 +96,7 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 #define PT_SLAB32 1  // the large-tree builds' BVH slab test in f32 with a conservative widening (C5 +1.3 %, r4f)
 #endif
 #ifndef PT_RECT_SIGN
-#define PT_RECT_SIGN 1  // rectangles: rays moving away from the plane rejected before the division (round 5)
+#define PT_RECT_SIGN 0  // rectangles: rays moving away from the plane rejected before the division (round 5 A/B: C2 2061 -> 2034, off)
 #endif
 #ifndef PT_AXIS_LEAF
 #define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,

@@ -803,17 +803,14 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             PT_MTRACE(guess, B, good, bmax);
             if (em && good >= ub) return M_MISS;
             good = good > bmax ? bmax : good;
-            if (good < 2.0) {
-                // no block proven: the crossing (or the range end) is inside the proof's margin, the band where
-                // f64 rounding of f can decide either way, and only literal steps get through it.  Each failed
-                // attempt in a row doubles the literal batch, so a march that grazes the surface over tens of
-                // steps pays for a few proofs, not one per step (round 5: jobs of >= 63 iterations 140 -> ...)
-                nlit = LIT_BATCH << (m.lit < LIT_DOUBLINGS ? m.lit : LIT_DOUBLINGS);
-                m.lit++;
-                goto literal;
-            }
-            m.lit = 0;
-            {
+            // no block proven (good < 2): the crossing (or the range end) is inside the proof's margin, the band
+            // where f64 rounding of f can decide either way, and only literal steps get through it.  Each failed
+            // attempt in a row doubles the literal batch, so a march that grazes the surface over tens of steps
+            // pays for a few proofs, not one per step (round 5: the longest captured job 63+ -> 22 iterations).
+            // (Selects, not a branch: a branch here spilled an exec mask of the march kernel.)
+            nlit = good >= 2.0 ? nlit : LIT_BATCH << (m.lit < LIT_DOUBLINGS ? m.lit : LIT_DOUBLINGS);
+            m.lit = good >= 2.0 ? 0 : m.lit + 1;
+            if (good >= 2.0) {
                 // the block's exact advance runs one binade segment per
                 // coordinate per iteration (march_advance), so a lane whose
                 // coordinates cross many binades does not stall its wave

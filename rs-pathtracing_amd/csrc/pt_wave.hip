@@ -272,6 +272,10 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
 constexpr int WF_PREDICT = 4;
 
+#ifndef PT_MARCH_SPREAD
+#define PT_MARCH_SPREAD 1  // a short march queue dealt in runs of count / blocks (1), or always in slice runs (0)
+#endif
+
 #ifndef PT_WAVE_COMPACT
 #define PT_WAVE_COMPACT 1  // bounce outputs compacted per wave (survivors first): 1 on, 0 every input position stored
 #endif
@@ -820,7 +824,7 @@ __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob 
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
 template <bool DIAG, int FK = march::F_ANY>
 __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs *__restrict__ A, int it,
-                                                                   unsigned long long *diag, uint32_t slice) {
+                                                                   unsigned long long *diag, uint32_t slice_max) {
     __shared__ uint32_t head;
     const WfArgs &a0 = kargs(A);
     const int nm = a0.sc.nmarch;
@@ -830,7 +834,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
     // pos(q).  slice == 0: one contiguous slice of the queue per block.
     // slice > 0: runs of `slice` consecutive jobs dealt round-robin to the
     // blocks, so a heavy region of the (pixel-sorted) queue is shared by many
-    // blocks while each run stays pixel-coherent.
+    // blocks while each run stays pixel-coherent.  A queue shorter than
+    // slice_max runs per block is dealt in shorter runs (count / blocks), so
+    // the few jobs of a late iteration spread over the CUs instead of sharing
+    // one block's waves: each wave's trips then cost only its own jobs' code
+    // (a persistent launch lasts as long as its slowest wave; round 5).
+    const uint32_t slice = slice_max == 0 ? 0u
+                           : (PT_MARCH_SPREAD && count / gridDim.x < slice_max ? max(1u, count / gridDim.x) : slice_max);
     uint32_t per, lo;
     if (slice == 0) {
         per = (count + gridDim.x - 1) / gridDim.x;
@@ -1195,11 +1205,16 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
         wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
-    if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH (C5): the FMA slab build
-        if (sc.nmarch == 0)  // (C5) no marched shape: no march pre-check or Heart code in the build
-            wf_bounce<NW, FIRST, 3, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it);
-        else
-            wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
+    if (sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0) {  // a large BVH and no marched shape (C5): the FMA slab
+        switch (waves) {                                   // build without march pre-check or Heart code
+        case 4: wf_bounce<NW, FIRST, 4, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 5: wf_bounce<NW, FIRST, 5, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        default: wf_bounce<NW, FIRST, 3, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        }
+        return;
+    }
+    if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH with a marched shape
+        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves
@@ -1321,7 +1336,8 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         // least wf_min_chunks sample chunks, so the pipelined slots overlap one
         // chunk's short tail iterations with the next chunk's work; chunks
         // keep at least MIN_CHUNK_PATHS paths to fill the device.
-        const uint32_t mc = (uint32_t)tu.wf_min_chunks;
+        // (a progressive frame's band, P0.stop set, gets at least two: one per chunk stream)
+        const uint32_t mc = P0.stop && tu.wf_min_chunks < 2 ? 2u : (uint32_t)tu.wf_min_chunks;
         if (mc > 1 && ntiles <= group_tiles) {
             uint32_t want = (nsw + mc - 1) / mc;
             const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;

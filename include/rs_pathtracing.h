@@ -348,7 +348,8 @@ int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches,
  * loads, shade, unwind, trace, march pre-check, stores; each section ended by
  * a full s_waitcnt, so the waits it causes are charged to it) — and turns the
  * instrumented build on (enable = 1) or off.  PT_ERR_STATE while a
- * render_start frame is in flight. */
+ * render_start frame is in flight; PT_ERR_UNSUPPORTED (enable = 1) unless the
+ * library was built with the instrumentation (make EXTRA=-DPT_WAVE_DIAG=1). */
 int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n);
 
 /* Diagnostic: render the whole frame (depth <= 8) with a timing build of the

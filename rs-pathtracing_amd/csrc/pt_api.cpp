@@ -1117,6 +1117,8 @@ int pt_wave_diag(pt_renderer *r, int enable, uint64_t *out, size_t n) {
     if (!r) return fail(PT_ERR_INVALID, "null argument");
     // the band feeder may queue launches that use the diag buffer
     if (r->started) return fail(PT_ERR_STATE, "a progressive frame is in flight (render_step it to the end or stop it)");
+    if (enable && !PT_WAVE_DIAG)
+        return fail(PT_ERR_UNSUPPORTED, "wave diagnostics are compiled out of this build (make EXTRA=-DPT_WAVE_DIAG=1)");
     HIP_TRY(hipSetDevice(r->device()));
     HIP_TRY(hipStreamSynchronize(r->stream()));
     if (out && n && r->gpus[0].ws.diag) HIP_TRY(hipMemcpy(out, r->gpus[0].ws.diag, (n < 64 ? n : 64) * 8, hipMemcpyDeviceToHost));

@@ -277,7 +277,7 @@ static dev::Scene dscene(const DeviceScene &s) {
 
 // ------------------------------------------------------------- tuning
 const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
-                                    "wf_bounce_waves", "wf_fused", "wf_march_slice", "wf_trace_slice",
+                                    "wf_bounce_waves", "wf_march_slice",
                                     "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "bvh_leaf", nullptr};
 
 static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
@@ -293,9 +293,7 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         {"wf_slots", &Tuning::wf_slots, 1, WaveWorkspace::MAX_SLOTS},
         {"wf_min_chunks", &Tuning::wf_min_chunks, 1, 4096},
         {"wf_bounce_waves", &Tuning::wf_bounce_waves, 2, 8},
-        {"wf_fused", &Tuning::wf_fused, 0, 1},
         {"wf_march_slice", &Tuning::wf_march_slice, 0, 1 << 20},
-        {"wf_trace_slice", &Tuning::wf_trace_slice, 1, 1 << 20},
         {"wf_march_blocks_per_cu", &Tuning::wf_march_blocks_per_cu, 0, 64},
         {"wf_side_priority", &Tuning::wf_side_priority, -1, 1},
         {"wf_pingpong", &Tuning::wf_pingpong, 0, 3},

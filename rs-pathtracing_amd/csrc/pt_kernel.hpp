@@ -48,9 +48,7 @@ struct Tuning {
     int64_t wf_paths = 3 << 24;      // path slots per chunk (256 .. 2^28); 48M: 24 spp of 1080p (24M: 1795, 32M: 1818, 48M: 1830, 64M: 1832 M samples/s)
     int wf_min_chunks = 1;           // at least this many sample chunks per frame (1..4096)
     int wf_bounce_waves = 3;         // wf_bounce register budget (2, 3, 4, 5, 6, 8)
-    int wf_fused = 0;                // fused bounces (wf_trace) instead of one launch per bounce
     int wf_march_slice = 256;        // march-queue run dealt to a block (0 = contiguous share)
-    int wf_trace_slice = 256;        // live-list run dealt to a wf_trace block
     int wf_march_blocks_per_cu = 0;  // persistent march grid (0 = occupancy maximum)
     int wf_side_priority = 0;        // the library's chunk streams' priority (-1 low, 0 normal, 1 high)
     int wf_pingpong = 0;             // bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
@@ -61,6 +59,13 @@ Tuning tuning_defaults();  // the measured defaults; a renderer changes them onl
 int tuning_set(Tuning *t, const char *name, int64_t value);
 int tuning_get(const Tuning &t, const char *name, int64_t *value);
 extern const char *const TUNING_NAMES[];  // null-terminated
+
+// Diagnostic builds of the wavefront kernels (pt_wave_diag: wave-level s_memtime per bounce section and march
+// phase): make EXTRA=-DPT_WAVE_DIAG=1.  In the product build the instrumentation is compiled out of every
+// kernel (it is no template parameter of the hot kernels) and pt_wave_diag refuses to enable it.
+#ifndef PT_WAVE_DIAG
+#define PT_WAVE_DIAG 0
+#endif
 
 struct WaveWorkspace {
     Tuning tune;  // this renderer's knobs (both engines read them from here)

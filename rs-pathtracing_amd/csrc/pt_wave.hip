@@ -63,13 +63,25 @@ using dev::V3;
 // field sits at an immediate offset from one per-lane address: with one array
 // per field the loop-invariant field bases of the two sets were 22 SGPR pairs,
 // and the bounce kernel spilled 65 SGPRs to VGPR lanes (round 5).
+#ifndef PT_PACK_META
+#define PT_PACK_META 1  // who and the attenuation-stack count in one word, the depth from the iteration (72 B state)
+#endif
+// PT_PACK_META: a live path's depth at bounce `it` is depth - (it - 1) for every path (each bounce before it
+// shaded it once and scattered), so only the stack count is state; it shares a word with the pending hit's
+// shape: (who + 1) | count << 25 (shapes < 2^24: the BVH's leaf index bound; count <= depth <= 64).
+constexpr uint32_t WHO_MASK = (1u << 25) - 1u;
+__host__ __device__ __forceinline__ uint32_t pack_who(int who, uint32_t count) {
+    return (uint32_t)(who + 1) | (count << 25);
+}
+__host__ __device__ __forceinline__ int unpack_who(uint32_t w) { return (int)(w & WHO_MASK) - 1; }
+
 struct PathSoA {
     char *base;
     size_t cap;  // a multiple of 64
-    static constexpr size_t BYTES = 8 * 8 + 3 * 4;  // per path
+    static constexpr size_t BYTES = 8 * 8 + (PT_PACK_META ? 2 : 3) * 4;  // per path
     static constexpr uint32_t BLK = 64, BLK_BYTES = (uint32_t)BYTES * BLK;
     enum F8 : int { OX, OY, OZ, DX, DY, DZ, T, RNG };
-    enum F4 : int { WHO, META, SID };
+    enum F4 : int { WHO, SID, META };  // (META: without PT_PACK_META only)
     // the 8-byte fields of position k: d8(k)[f * 64]; the 4-byte ones: d4(k)[f * 64]
     __host__ __device__ double *d8(uint32_t k) const {
         return (double *)(base + (size_t)(k / BLK) * BLK_BYTES) + (k % BLK);
@@ -78,7 +90,8 @@ struct PathSoA {
         return (uint32_t *)(base + (size_t)(k / BLK) * BLK_BYTES + 8 * 8 * BLK) + (k % BLK);
     }
     __host__ __device__ double &t(uint32_t k) const { return d8(k)[T * BLK]; }  // best hit t
-    __host__ __device__ int32_t &who(uint32_t k) const { return *(int32_t *)&d4(k)[WHO * BLK]; }  // best hit shape (-1: miss)
+    // the word holding the best hit's shape (-1: miss; PT_PACK_META: packed with the stack count, pack_who)
+    __host__ __device__ uint32_t &who(uint32_t k) const { return d4(k)[WHO * BLK]; }
 };
 
 // Device view of the workspace for one chunk.
@@ -220,8 +233,9 @@ template <typename T>
 __device__ __forceinline__ T ld_path(const T *p) {
     return *p;
 }
+// depth, count: the path's depth and attenuation-stack count (PT_PACK_META stores only the count, with who)
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
-                                           int who, uint64_t rng, uint32_t meta) {
+                                           int who, uint64_t rng, uint32_t depth, uint32_t count) {
     double *a = S.d8(k);
     uint32_t *b = S.d4(k);
     constexpr uint32_t B = PathSoA::BLK;
@@ -232,14 +246,16 @@ __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_
     st_path(a + PathSoA::DY * B, ray.d.y);
     st_path(a + PathSoA::DZ * B, ray.d.z);
     st_path(a + PathSoA::T * B, best);
-    st_path(b + PathSoA::WHO * B, (uint32_t)who);
+    st_path(b + PathSoA::WHO * B, PT_PACK_META ? pack_who(who, count) : (uint32_t)who);
     st_path((uint64_t *)a + PathSoA::RNG * B, (uint64_t)rng);
-    st_path(b + PathSoA::META * B, meta);
+    if (!PT_PACK_META) st_path(b + PathSoA::META * B, depth | count << 8);
     st_path(b + PathSoA::SID * B, id);
 }
-// The state of position p: slot id, ray, rng, meta, pending hit (who, t).
+// The state of position p: slot id, ray, rng, pending hit (who, t), attenuation-stack count, and the depth
+// (PT_PACK_META: depth_it, the depth of every path at this bounce).
 __device__ __forceinline__ void load_path(const PathSoA &S, uint32_t p, uint32_t *id, Ray *ray, uint64_t *rng,
-                                          uint32_t *meta, int *who, double *best) {
+                                          uint32_t depth_it, uint32_t *depth, uint32_t *count, int *who,
+                                          double *best) {
     const double *a = S.d8(p);
     const uint32_t *b = S.d4(p);
     constexpr uint32_t B = PathSoA::BLK;
@@ -247,8 +263,17 @@ __device__ __forceinline__ void load_path(const PathSoA &S, uint32_t p, uint32_t
     ray->o = dev::v3(ld_path(a + PathSoA::OX * B), ld_path(a + PathSoA::OY * B), ld_path(a + PathSoA::OZ * B));
     ray->d = dev::v3(ld_path(a + PathSoA::DX * B), ld_path(a + PathSoA::DY * B), ld_path(a + PathSoA::DZ * B));
     *rng = ld_path((const uint64_t *)a + PathSoA::RNG * B);
-    *meta = ld_path(b + PathSoA::META * B);
-    *who = (int)ld_path(b + PathSoA::WHO * B);
+    const uint32_t w = ld_path(b + PathSoA::WHO * B);
+    if (PT_PACK_META) {
+        *who = unpack_who(w);
+        *count = w >> 25;
+        *depth = depth_it;
+    } else {
+        const uint32_t meta = ld_path(b + PathSoA::META * B);
+        *who = (int)w;
+        *count = meta >> 8;
+        *depth = meta & 0xffu;
+    }
     *best = ld_path(a + PathSoA::T * B);
 }
 
@@ -289,8 +314,7 @@ constexpr int WF_PREDICT = 4;
 // full s_waitcnt so the memory waits it causes are charged to it (tuning
 // only): list load, state loads, shade, unwind, trace, march pre-check,
 // stores; summed into diag[36..42].
-template <int NW, bool FIRST, int WAVES, bool DIAG = false, int FK = march::F_ANY, bool EXT = false,
-          bool BIGBVH = false>
+template <int NW, bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false, bool BIGBVH = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict__ A, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -303,6 +327,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
         if (a.P.stop && blockIdx.x == 0 && threadIdx.x == 0 && v.cnt[3]) dev::note_stop(a.sc.guard, count > 0);
     }
     const uint32_t stride = gridDim.x * blockDim.x;
+    const bool DIAG = PT_WAVE_DIAG && diag;  // (a diagnostics build with pt_wave_diag enabled)
     unsigned long long dsec[7] = {0, 0, 0, 0, 0, 0, 0}, tst = 0;
     PT_LP_BEGIN();
 #define PT_BSTAMP(k)                                                \
@@ -345,11 +370,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
             } else {
                 const uint32_t p = v.list[i];
                 PT_BSTAMP(0)
-                uint32_t meta;
-                load_path(v.in, p, &id, &ray, &rng.s, &meta, &who, &best);
-                depth = meta & 0xffu;
+                uint32_t count;
+                // (every live path has been shaded it - 1 times, each a scatter: its depth is P.depth - (it - 1))
+                load_path(v.in, p, &id, &ray, &rng.s, P.depth + 1u - (uint32_t)it, &depth, &count, &who, &best);
                 stk.base = v.ids + id;
-                stk.n = (int)(meta >> 8);
+                stk.n = (int)count;
                 if (EXT) stk.vb = v.att + id;
                 PT_BSTAMP(1)
             }
@@ -451,7 +476,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
         }
         if (i < count) PT_LP(STORE);
         if (i < count && (!PT_WAVE_COMPACT || live)) {
-            store_path(v.out, k, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
+            store_path(v.out, k, id, ray, best, who, rng.s, depth, (uint32_t)stk.n);
             v.status[k] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         }
         PT_BSTAMP(6)
@@ -460,122 +485,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
     PT_LP_END();
     if (DIAG && (threadIdx.x & 63) == 0)
         for (int k = 0; k < 7; k++) atomicAdd(&diag[36 + k], dsec[k]);
-}
-
-// Fused bounces (PT_WF_FUSED=1; measured slower, see fused_bounces()): a lane carries its path through as
-// many bounces as it can without a march — shade the pending hit, trace the
-// new ray, and if no marched shape's bound starts before the best hit, shade
-// that hit at once in registers and go on.  Path state goes to HBM only when
-// the path needs a march (status 3: it joins the march queue and, after the
-// march, the next iteration's live list) or ends (its sample radiance).  The
-// grid is persistent: lanes whose path is done take the next path from the
-// block's runs of the input list (runs of `slice` ids dealt round-robin to the
-// blocks, an LDS head), so long paths do not hold finished lanes idle.  The
-// per-path sequence of operations is wf_bounce's, so the frame is the same
-// bit for bit; only paths that never meet a march skip the per-bounce state
-// round trip through HBM and the per-bounce launch.
-template <bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false>
-__global__ __launch_bounds__(256, WAVES) void wf_trace(const WfArgs *__restrict__ A, int it, uint32_t slice) {
-    __shared__ uint32_t head;
-    uint32_t count;
-    {
-        const WfView &v = kargs(A).v;
-        count = FIRST ? (v.cnt[3] ? 0u : v.ns * v.npix) : v.cnt[it * 4 + 0];
-    }
-    const uint32_t G = gridDim.x;
-    const uint32_t runs = (count + slice - 1) / slice;
-    const uint32_t per = (runs > blockIdx.x ? (runs - blockIdx.x + G - 1) / G : 0u) * slice;
-    auto pos = [&](uint32_t q) -> uint32_t { return (q / slice * G + blockIdx.x) * slice + q % slice; };
-    if (threadIdx.x == 0) head = blockDim.x;
-    __syncthreads();
-    uint32_t q = threadIdx.x;
-    bool have = q < per && pos(q) < count;
-    bool fresh = true;
-    uint32_t id = 0, k = 0, depth = 0;  // slot id, input (= output) position
-    Ray ray;
-    ray.o = ray.d = dev::v3(0.0, 0.0, 0.0);
-    dev::Rng rng{0};
-    MemStack stk{nullptr, 0, 0, nullptr};
-    double best = 0.0;
-    int who = -1;
-    while (have) {
-        const WfArgs &a = kargs(A);
-        const dev::Scene &sc = a.sc;
-        const FrameParams &P = a.P;
-        const WfView &v = a.v;
-        stk.stride = v.cap;
-        bool done = false, shade_now = true;
-        if (fresh) {
-            fresh = false;
-            k = pos(q);
-            if (FIRST) {
-                shade_now = false;
-                id = k;
-                uint32_t x, y, sl, pl;
-                slot_pixel(P, v, id, &x, &y, &sl, &pl);
-                if (x >= P.width || y >= P.height || sl >= v.ns) {
-                    v.status[k] = 0;
-                    done = true;
-                } else {
-                    rng.s = dev::sample_key(P.seed, (uint64_t)x + (uint64_t)y * P.width, v.s0 + sl);
-                    ray = dev::camera_ray(P, x, y, rng);
-                    depth = P.depth;
-                    stk.base = v.ids + id;
-                    stk.n = 0;
-                    if (EXT) stk.vb = v.att + id;
-                }
-            } else {
-                const uint32_t p = v.list[k];
-                uint32_t meta;
-                load_path(v.in, p, &id, &ray, &rng.s, &meta, &who, &best);
-                depth = meta & 0xffu;
-                stk.base = v.ids + id;
-                stk.n = (int)(meta >> 8);
-                if (EXT) stk.vb = v.att + id;
-            }
-        }
-        if (!done && shade_now) {
-            V3 leaf;
-            if (dev::shade<false, FK, EXT>(sc, who, best, ray, depth, stk, rng, P.s11, &leaf)) {
-                end_path(v, id, stk, leaf);
-                v.status[k] = 0;
-                done = true;
-            }
-        }
-        if (!done) {
-            const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-            best = __builtin_inf();
-            who = -1;
-            dev::closest_nomarch<false, EXT>(sc, ray, inv, T_MIN, &best, &who);
-            bool need_march = false;
-            for (int km = 0; km < sc.nmarch && !need_march; km++) {
-                const int s = dev::uniform_load(&sc.march[km]);
-                const DBox b = dev::uniform_box(&sc.boxes[s]);
-                if (!dev::slab(b.lo, b.hi, ray, inv, T_MIN, best)) continue;
-                const DShape S = dev::uniform_shape(&sc.shapes[s]);
-                const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
-                double st, en;
-                need_march = march::shape_bound_k<FK>(dev::shape_params(S), o.x, o.y, o.z, d.x, d.y, d.z, &st, &en);
-                if (need_march && v.jo) {
-                    double2 *j = v.jo + (size_t)k * 4;
-                    j[0] = make_double2(o.x, o.y);
-                    j[1] = make_double2(o.z, d.x);
-                    j[2] = make_double2(d.y, d.z);
-                    j[3] = make_double2(st, en);
-                }
-            }
-            if (need_march) {
-                store_path(v.out, k, id, ray, best, who, rng.s, depth | ((uint32_t)stk.n << 8));
-                v.status[k] = 3;
-                done = true;
-            }
-        }
-        if (done) {
-            q = atomicAdd(&head, 1u);
-            have = q < per && pos(q) < count;
-            fresh = true;
-        }
-    }
 }
 
 // Order-preserving compaction of the status bytes into the two position lists
@@ -807,7 +716,15 @@ struct MarchJob {
     Ray ray;
     double best;
     int who;
+    uint32_t hi;  // PT_PACK_META: the stack-count bits of the who word, written back unchanged
 };
+__device__ __forceinline__ void job_who(MarchJob *j, uint32_t w) {
+    j->who = PT_PACK_META ? unpack_who(w) : (int)w;
+    j->hi = PT_PACK_META ? (w & ~WHO_MASK) : 0u;
+}
+__device__ __forceinline__ uint32_t job_who_word(int who, uint32_t hi) {
+    return PT_PACK_META ? (uint32_t)(who + 1) | hi : (uint32_t)who;
+}
 
 __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob *j) {
     const double *a = S.d8(p);
@@ -816,16 +733,17 @@ __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob 
     j->ray.o = dev::v3(a[PathSoA::OX * B], a[PathSoA::OY * B], a[PathSoA::OZ * B]);
     j->ray.d = dev::v3(a[PathSoA::DX * B], a[PathSoA::DY * B], a[PathSoA::DZ * B]);
     j->best = S.t(p);
-    j->who = S.who(p);
+    job_who(j, S.who(p));
 }
 
 // DIAG: per trip, the set of phase kinds present among the wave's lanes (bit
 // 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
-template <bool DIAG, int FK = march::F_ANY>
+template <int FK = march::F_ANY>
 __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs *__restrict__ A, int it,
                                                                    unsigned long long *diag, uint32_t slice_max) {
     __shared__ uint32_t head;
+    const bool DIAG = PT_WAVE_DIAG && diag;  // (a diagnostics build with pt_wave_diag enabled)
     const WfArgs &a0 = kargs(A);
     const int nm = a0.sc.nmarch;
     const uint32_t count = a0.v.cnt[it * 4 + 1];
@@ -883,7 +801,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
         if (pre) {
             cur.id = id;
             cur.best = v.out.t(id);
-            cur.who = v.out.who(id);
+            job_who(&cur, v.out.who(id));
             const double2 *j = v.jo + (size_t)id * 4;
             const double2 a = j[0], b = j[1], c = j[2], e = j[3];
             march::march_start<FK>(F0, step0, passes0, a.x, a.y, b.x, b.y, c.x, c.y, e.x, e.y, &ms);
@@ -967,7 +885,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
                 // results are stored after the next job's loads are issued
                 const uint32_t fid = cur.id;
                 const double fbest = cur.best;
-                const int fwho = cur.who;
+                const uint32_t fwho = job_who_word(cur.who, cur.hi);
                 const WfView &v = kargs(A).v;
                 q = atomicAdd(&head, 1u);
                 have = q < per && pos(q) < count;
@@ -1190,40 +1108,40 @@ template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it,
                           unsigned long long *diag, int fkind, int waves) {
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
-        wf_bounce<NW, FIRST, 2, false, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<NW, FIRST, 2, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (fkind != march::F_HEART) {  // another ray-marched function: the generic build
-        wf_bounce<NW, FIRST, 2, false, march::F_ANY><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<NW, FIRST, 2, march::F_ANY><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
-    if (diag) {
-        wf_bounce<NW, FIRST, 2, true, march::F_HEART><<<blocks, 256, 0, st>>>(A, it, diag);
+    if (PT_WAVE_DIAG && diag) {  // (diagnostics builds)
+        wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it, diag);
         return;
     }
     if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
-        wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0) {  // a large BVH and no marched shape (C5): the FMA slab
         switch (waves) {                                   // build without march pre-check or Heart code
-        case 4: wf_bounce<NW, FIRST, 4, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
-        case 5: wf_bounce<NW, FIRST, 5, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
-        default: wf_bounce<NW, FIRST, 3, false, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 4: wf_bounce<NW, FIRST, 4, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 5: wf_bounce<NW, FIRST, 5, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        default: wf_bounce<NW, FIRST, 3, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
         }
         return;
     }
     if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH with a marched shape
-        wf_bounce<NW, FIRST, 3, false, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<NW, FIRST, 3, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves
-    case 2: wf_bounce<NW, FIRST, 2, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 4: wf_bounce<NW, FIRST, 4, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 5: wf_bounce<NW, FIRST, 5, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 6: wf_bounce<NW, FIRST, 6, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 8: wf_bounce<NW, FIRST, 8, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    default: wf_bounce<NW, FIRST, 3, false, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 2: wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 4: wf_bounce<NW, FIRST, 4, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 5: wf_bounce<NW, FIRST, 5, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 6: wf_bounce<NW, FIRST, 6, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 8: wf_bounce<NW, FIRST, 8, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    default: wf_bounce<NW, FIRST, 3, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
     }
 }
 
@@ -1237,26 +1155,6 @@ static uint32_t resident_blocks(K kern) {
     }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0) != hipSuccess || occ < 1) occ = 1;
     return (uint32_t)(cus * occ);
-}
-
-// The fused bounce step (wf_trace) only with Tuning::wf_fused.  Measured on C2:
-// 1119 M samples/s fused against 1176 with one wf_bounce launch per bounce —
-// the bounce is VALU-bound, not bound by the path-state traffic fusion
-// removes, and the per-bounce launches interleave better with the other
-// chunk's marches — so per-bounce launches are the default.  The diag build
-// always runs wf_bounce.
-template <bool FIRST>
-static void launch_trace(hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it, int fkind, uint32_t slice) {
-    if (sc.ext) {
-        static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY, true>);
-        wf_trace<FIRST, 2, march::F_ANY, true><<<nb, 256, 0, st>>>(A, it, slice);
-    } else if (fkind != march::F_HEART) {
-        static const uint32_t nb = resident_blocks(wf_trace<FIRST, 2, march::F_ANY>);
-        wf_trace<FIRST, 2, march::F_ANY><<<nb, 256, 0, st>>>(A, it, slice);
-    } else {
-        static const uint32_t nb = resident_blocks(wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART>);
-        wf_trace<FIRST, PT_WF_BOUNCE_WAVES, march::F_HEART><<<nb, 256, 0, st>>>(A, it, slice);
-    }
 }
 
 // Chunks in flight (Tuning::wf_slots): each has its own path state (slot) and
@@ -1405,7 +1303,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
 
     // persistent march grid: exactly the resident blocks of the device (or
     // Tuning::wf_march_blocks_per_cu per CU, if fewer)
-    static const uint32_t march_resident = resident_blocks(wf_march<false, march::F_HEART>);
+    static const uint32_t march_resident = resident_blocks(wf_march<march::F_HEART>);
     uint32_t march_blocks = march_resident;
     if (tu.wf_march_blocks_per_cu > 0) {
         int dev = 0, cus = 256;
@@ -1415,7 +1313,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         if (want < march_blocks) march_blocks = want;
     }
     const uint32_t march_slice = (uint32_t)tu.wf_march_slice;
-    const bool fused = tu.wf_fused && !ws->diag;
     // Chunks run in rounds of `slots`, chunk j of a round on stream j, and are
     // enqueued iteration by iteration across the round.  With wf_pingpong the
     // bounce launches form one chain across the streams (each waits for the
@@ -1497,13 +1394,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
-                if (it == 0) {
-                    if (fused) launch_trace<true>(cs, sc, A, 0, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves);
-                } else {
-                    if (fused) launch_trace<false>(cs, sc, A, it, fkind, (uint32_t)tu.wf_trace_slice);
-                    else launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves);
-                }
+                if (it == 0)
+                    launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves);
+                else
+                    launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (pingpong) {
@@ -1528,11 +1422,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)
-                    wf_march<false, march::F_ANY><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
+                    wf_march<march::F_ANY><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
                 else if (ws->diag)
-                    wf_march<true, march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, ws->diag, march_slice);
+                    wf_march<march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, ws->diag, march_slice);
                 else
-                    wf_march<false, march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
+                    wf_march<march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (mchain) {

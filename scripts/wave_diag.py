@@ -1,4 +1,7 @@
-"""Phase diagnostics of the wavefront march kernel on one frame (tuning)."""
+"""Phase diagnostics of the wavefront march kernel on one frame (tuning).  Needs a diagnostics build of the
+library (the product build compiles the instrumentation out):
+    make -C rs-pathtracing_amd LIB=../variants/diag.so BUILD=build_diag EXTRA=-DPT_WAVE_DIAG=1
+    PT_AMD_LIB=variants/diag.so python scripts/wave_diag.py [spp]"""
 import os, sys
 sys.path.insert(0, os.getcwd())
 import numpy as np

@@ -355,6 +355,9 @@ def test_diagnostics_refused_while_a_frame_is_in_flight(pt, cornell):
         pass
     pt.kernel_timing(r, False)  # allowed again once the frame is done
     assert pt.march_guard_drops(r) == 0
+    with pytest.raises(pt.PtError) as e:  # the product build carries no wave instrumentation
+        pt.wave_diag(r, True)
+    assert e.value.code == pt.PT_ERR_UNSUPPORTED
     sampled_rows_check(osc, buf, w, h, 8, np.arange(h), n=512, seed=3)
 
 

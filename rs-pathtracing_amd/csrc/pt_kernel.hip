@@ -278,7 +278,7 @@ static dev::Scene dscene(const DeviceScene &s) {
 // ------------------------------------------------------------- tuning
 const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
                                     "wf_bounce_waves", "wf_march_slice",
-                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "bvh_leaf", nullptr};
+                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "bvh_leaf", nullptr};
 
 static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
     struct F {
@@ -297,6 +297,7 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         {"wf_march_blocks_per_cu", &Tuning::wf_march_blocks_per_cu, 0, 64},
         {"wf_side_priority", &Tuning::wf_side_priority, -1, 1},
         {"wf_pingpong", &Tuning::wf_pingpong, 0, 3},
+        {"wf_stagger", &Tuning::wf_stagger, 0, 1},
         {"bvh_leaf", &Tuning::bvh_leaf, 1, 16},
     };
     *iv = nullptr;
@@ -305,6 +306,11 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         *lo = 256;
         *hi = (int64_t)1 << 28;
         return &t->wf_paths;
+    }
+    if (!strcmp(name, "wf_tail_paths")) {
+        *lo = 0;
+        *hi = (int64_t)1 << 28;
+        return &t->wf_tail_paths;
     }
     for (const F &f : fs)
         if (!strcmp(name, f.n)) {

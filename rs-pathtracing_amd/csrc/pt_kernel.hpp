@@ -29,7 +29,7 @@ struct DeviceScene {
 // reused by every frame of a renderer.
 // Per-kernel launch timing (pt_kernel_timing): HIP events recorded on the
 // launch stream around every render-path kernel while enabled.
-enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_KINDS = 5 };
+enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_TAIL = 5, K_KINDS = 6 };
 struct KernelTimer;
 KernelTimer *timer_new();
 void timer_free(KernelTimer *t);
@@ -52,6 +52,8 @@ struct Tuning {
     int wf_march_blocks_per_cu = 0;  // persistent march grid (0 = occupancy maximum)
     int wf_side_priority = 0;        // the library's chunk streams' priority (-1 low, 0 normal, 1 high)
     int wf_pingpong = 0;             // bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
+    int wf_stagger = 0;              // 1: chunk streams offset by 1/slots of a chunk (staggered sample chunks; C2 -1.2 %, depth 50 -3 %)
+    int64_t wf_tail_paths = 0;       // a chunk's live paths from which wf_tail runs them to their ends (0 = never)
     int bvh_leaf = 1;                // shapes per BVH leaf (1..16; C5 677 / 609 / 534 M samples/s at 1 / 2 / 4)
 };
 Tuning tuning_defaults();  // the measured defaults; a renderer changes them only through pt_renderer_set_option

@@ -301,6 +301,10 @@ constexpr int WF_PREDICT = 4;
 #define PT_MARCH_SPREAD 1  // a short march queue dealt in runs of count / blocks (1), or always in slice runs (0)
 #endif
 
+#ifndef PT_MARCH_WAVE_RUNS
+#define PT_MARCH_WAVE_RUNS 1  // a march queue shorter than the grid's lanes dealt one run per wave (1), or per block (0)
+#endif
+
 #ifndef PT_WAVE_COMPACT
 #define PT_WAVE_COMPACT 1  // bounce outputs compacted per wave (survivors first): 1 on, 0 every input position stored
 #endif
@@ -537,11 +541,10 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t x, uint32_t *total, ui
 
 // The thread's 16 statuses; positions at or past the bounce's input count n
 // (stale bytes of earlier iterations) read as 0.
-__device__ __forceinline__ uint4 cp_load(const uint8_t *__restrict__ st, const uint32_t *n_dev, uint32_t n_host) {
-    const uint32_t n = n_dev ? *n_dev : n_host;
-    const uint32_t b = blockIdx.x * CP_TILE + threadIdx.x * CP_ITEMS;
+__device__ __forceinline__ uint4 cp_load(const uint8_t *__restrict__ st, uint32_t tile, uint32_t n) {
+    const uint32_t b = tile * CP_TILE + threadIdx.x * CP_ITEMS;
     if (b >= n) return make_uint4(0u, 0u, 0u, 0u);
-    uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)blockIdx.x * CP_TILE)[threadIdx.x];
+    uint4 q = reinterpret_cast<const uint4 *>(st + (size_t)tile * CP_TILE)[threadIdx.x];
     if (n - b < (uint32_t)CP_ITEMS) {
         const uint32_t k = n - b;  // bytes kept: 1 .. 15
         uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -570,21 +573,34 @@ struct CpLayout {
     __device__ uint32_t at(uint32_t b) const { return (b % per) * CP_BLOCK + b / per; }
 };
 
+// The compaction kernels cover the tiles of the bounce's input count n (read
+// on the device) with at most CP_GRID blocks, each looping over tiles: a late
+// iteration's few live paths no longer launch a grid of the chunk's size
+// (three launches of ~11k blocks cost ~40 us even with nothing to do, round 5).
+#ifndef PT_CP_GRID
+#define PT_CP_GRID 2048  // (0: one block per tile of the chunk, as before round 5)
+#endif
+constexpr uint32_t CP_GRID = PT_CP_GRID;
+__device__ __forceinline__ uint32_t cp_n(const uint32_t *n_dev, uint32_t n_host) { return n_dev ? *n_dev : n_host; }
+
 // per tile: (live, long march, short march) counts
 __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, uint32_t *__restrict__ blk, CpLayout L,
                                                 const uint32_t *__restrict__ n_dev, uint32_t n_host) {
     __shared__ uint32_t lds[12];
-    const uint4 q = cp_load(st, n_dev, n_host);
-    uint32_t l, m, g, tl, tg, ts;
-    cp_bits(q, &l, &m, &g);
-    block_exscan(l, &tl, lds);
-    block_exscan(g, &tg, lds + 4);
-    block_exscan(m - g, &ts, lds + 8);
-    if (threadIdx.x == 0) {
-        const uint32_t k = L.at(blockIdx.x);
-        blk[k] = tl;
-        blk[L.stride + k] = tg;
-        blk[2 * L.stride + k] = ts;
+    const uint32_t n = cp_n(n_dev, n_host), nt = (n + CP_TILE - 1) / CP_TILE;
+    for (uint32_t tb = blockIdx.x; tb < nt; tb += gridDim.x) {  // (block-uniform)
+        const uint4 q = cp_load(st, tb, n);
+        uint32_t l, m, g, tl, tg, ts;
+        cp_bits(q, &l, &m, &g);
+        block_exscan(l, &tl, lds);
+        block_exscan(g, &tg, lds + 4);
+        block_exscan(m - g, &ts, lds + 8);
+        if (threadIdx.x == 0) {
+            const uint32_t k = L.at(tb);
+            blk[k] = tl;
+            blk[L.stride + k] = tg;
+            blk[2 * L.stride + k] = ts;
+        }
     }
 }
 
@@ -594,10 +610,13 @@ __global__ __launch_bounds__(256) void cp_count(const uint8_t *__restrict__ st, 
 // the wave), loaded into registers up front (every load in flight together)
 // when the run is at most SCAN_RUN tiles, and the block scans once.
 constexpr int SCAN_RUN = 48;
-__global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk, CpLayout L,
+__global__ __launch_bounds__(256) void cp_scan(uint32_t *__restrict__ blk, uint32_t nblk_max, CpLayout L,
+                                               const uint32_t *__restrict__ n_dev, uint32_t n_host,
                                                uint32_t *__restrict__ n_live, uint32_t *__restrict__ n_march,
                                                uint32_t *__restrict__ n_long) {
     __shared__ uint32_t lds[12];
+    const uint32_t nt = (cp_n(n_dev, n_host) + CP_TILE - 1) / CP_TILE;
+    const uint32_t nblk = nt < nblk_max ? nt : nblk_max;  // the tiles cp_count wrote
     const uint32_t per = L.per;
     const uint32_t b0 = threadIdx.x * per;
     const uint32_t nj = b0 >= nblk ? 0u : (nblk - b0 < per ? nblk - b0 : per);  // this thread's tiles
@@ -672,31 +691,34 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
                                                   uint32_t n_host) {
     __shared__ uint32_t lds[12];
     __shared__ uint32_t ids[CP_TILE];  // the tile's live ids, then its march ids (long, then short)
-    const size_t base = (size_t)blockIdx.x * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
-    const uint4 q = cp_load(st, n_dev, n_host);
-    uint32_t l, m, g, tl, tg, ts;
-    cp_bits(q, &l, &m, &g);
-    uint32_t ol = block_exscan(l, &tl, lds);
-    uint32_t og = block_exscan(g, &tg, lds + 4);
-    uint32_t os = tg + block_exscan(m - g, &ts, lds + 8);
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    const uint32_t n = cp_n(n_dev, n_host), nt = (n + CP_TILE - 1) / CP_TILE;
+    for (uint32_t tb = blockIdx.x; tb < nt; tb += gridDim.x) {  // (block-uniform)
+        const size_t base = (size_t)tb * CP_TILE + (size_t)threadIdx.x * CP_ITEMS;
+        const uint4 q = cp_load(st, tb, n);
+        uint32_t l, m, g, tl, tg, ts;
+        cp_bits(q, &l, &m, &g);
+        uint32_t ol = block_exscan(l, &tl, lds);  // (its barriers also end the previous tile's reads of ids)
+        uint32_t og = block_exscan(g, &tg, lds + 4);
+        uint32_t os = tg + block_exscan(m - g, &ts, lds + 8);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int k = 0; k < CP_ITEMS; k++)
-        if ((w[k >> 2] >> (8 * (k & 3))) & 1u) ids[ol++] = (uint32_t)(base + k);
-    __syncthreads();
-    const uint32_t kb = L.at(blockIdx.x);
-    const uint32_t bl = blk[kb], bg = blk[L.stride + kb], bs = *n_long + blk[2 * L.stride + kb];
-    for (uint32_t k = threadIdx.x; k < tl; k += CP_BLOCK) live_out[bl + k] = ids[k];
-    if (tg + ts == 0) return;  // (block-uniform)
-    __syncthreads();
+        for (int k = 0; k < CP_ITEMS; k++)
+            if ((w[k >> 2] >> (8 * (k & 3))) & 1u) ids[ol++] = (uint32_t)(base + k);
+        __syncthreads();
+        const uint32_t kb = L.at(tb);
+        const uint32_t bl = blk[kb], bg = blk[L.stride + kb], bs = *n_long + blk[2 * L.stride + kb];
+        for (uint32_t k = threadIdx.x; k < tl; k += CP_BLOCK) live_out[bl + k] = ids[k];
+        if (tg + ts == 0) continue;  // (block-uniform)
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < CP_ITEMS; k++) {
-        const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-        if (b & 2u) ids[(b & 4u) ? og++ : os++] = (uint32_t)(base + k);
+        for (int k = 0; k < CP_ITEMS; k++) {
+            const uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+            if (b & 2u) ids[(b & 4u) ? og++ : os++] = (uint32_t)(base + k);
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < tg; k += CP_BLOCK) march_out[bg + k] = ids[k];
+        for (uint32_t k = threadIdx.x; k < ts; k += CP_BLOCK) march_out[bs + k] = ids[tg + k];
     }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < tg; k += CP_BLOCK) march_out[bg + k] = ids[k];
-    for (uint32_t k = threadIdx.x; k < ts; k += CP_BLOCK) march_out[bs + k] = ids[tg + k];
 }
 
 // Marches of iteration `it`.  Each workgroup owns a contiguous slice of the
@@ -777,8 +799,19 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
     if (slice == 0) per = hi > lo ? hi - lo : 0u;
     if (threadIdx.x == 0) head = blockDim.x;
     __syncthreads();
+    // A queue of fewer jobs than the grid has lanes (the late iterations) is
+    // dealt in runs of kw = ceil(count / waves) consecutive jobs, one run per
+    // wave (wave w of block b: run w * blocks + b), one job per lane and no
+    // refill: every wave of the grid takes part, each with the fewest jobs.  A
+    // trip of a wave costs the union of its lanes' march phases, and the launch
+    // lasts as long as its slowest wave: dealt per block, a late queue of ~10
+    // jobs per block put them all in the block's first wave (round 5).
+    const uint32_t nwv = blockDim.x >> 6;
+    const bool runs_w = PT_MARCH_WAVE_RUNS && slice_max != 0 && count < G * blockDim.x;
+    const uint32_t kw = runs_w ? (count + G * nwv - 1) / (G * nwv) : 0u;
+    const uint32_t pw = ((threadIdx.x >> 6) * G + blockIdx.x) * kw + (threadIdx.x & 63);
     uint32_t q = threadIdx.x;
-    bool have = q < per && pos(q) < count;
+    bool have = runs_w ? (threadIdx.x & 63) < kw && pw < count : q < per && pos(q) < count;
     // one marched shape and jobs pre-selected by the bounce kernel: a job is
     // its march alone (no select, no ray transform, no bound quadratic here)
     const bool pre = a0.v.jo != nullptr;
@@ -812,7 +845,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
         }
     };
     PT_MREG_KERNEL_BEGIN();
-    if (have) start_job(a0.v, pos(q));
+    if (have) start_job(a0.v, runs_w ? pw : pos(q));
     V3 inv = pre ? dev::v3(0.0, 0.0, 0.0) : dev::v3(1.0 / cur.ray.d.x, 1.0 / cur.ray.d.y, 1.0 / cur.ray.d.z);
     march::MarchStats mst{0, 0, 0, 0};
     unsigned long long dtrips[16], dcyc[16], dlanes[4];
@@ -887,9 +920,13 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
                 const double fbest = cur.best;
                 const uint32_t fwho = job_who_word(cur.who, cur.hi);
                 const WfView &v = kargs(A).v;
-                q = atomicAdd(&head, 1u);
-                have = q < per && pos(q) < count;
-                if (have) start_job(v, pos(q));
+                if (runs_w) {
+                    have = false;
+                } else {
+                    q = atomicAdd(&head, 1u);
+                    have = q < per && pos(q) < count;
+                    if (have) start_job(v, pos(q));
+                }
                 v.out.t(fid) = fbest;
                 v.out.who(fid) = fwho;
                 if (have && !pre) {
@@ -912,6 +949,123 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
             atomicAdd(&diag[16 + k], dcyc[k]);
         }
         for (int k = 0; k < 4; k++) atomicAdd(&diag[32 + k], dlanes[k]);
+    }
+}
+
+// The tail of a chunk (round 5).  The live paths of a chunk decay by ~10 %
+// per bounce; once few are left, each iteration's launches are latency-bound:
+// a persistent march launch lasts as long as its slowest job (~200-250 us at
+// depth 50, whatever the queue length), a bounce and its compaction ~60 us,
+// and a depth-50 chunk spent a quarter of its time in 30 such iterations
+// (profiles/r5/kt_iters_c2_depth50_final.txt).  wf_tail runs before the
+// bounce of iteration it: when that bounce's live list holds at most
+// max_paths paths, its persistent lanes take the paths one at a time and run
+// each to its end -- shade the pending hit, trace, select and march, shade
+// again, ... (trace_pixel's phase machine, dev::shade, the same march code as
+// wf_march's selecting path) -- storing the leaf record the reduce unwinds.  A
+// path's operations and values are the ones the per-iteration kernels would
+// have produced.  The last block to finish sets the live count of iteration
+// `it` to 0, so the chunk's remaining launches find no work.  cnt[it * 4 + 3]
+// (it >= 1: unused) is the path counter, cnt[it * 4 + 2] (rewritten by this
+// iteration's compaction) the finished-block counter.
+enum TailPhase : int { TP_TRACE = 0, TP_SELECT = 1, TP_MARCH = 2, TP_SHADE = 3 };
+#ifndef PT_WF_TAIL_WAVES
+#define PT_WF_TAIL_WAVES 2  // waves per SIMD the tail kernel's registers must allow
+#endif
+template <int FK, bool EXT, bool BIGBVH>
+__global__ __launch_bounds__(256, PT_WF_TAIL_WAVES) void wf_tail(const WfArgs *__restrict__ A, int it,
+                                                                 uint32_t max_paths) {
+    const uint32_t count = kargs(A).v.cnt[it * 4 + 0];
+    if (count == 0 || count > max_paths) return;  // (every block sees the same count)
+    {
+        const uint32_t depth_it = kargs(A).P.depth + 1u - (uint32_t)it;
+        bool have = false;
+        uint32_t id = 0, depth = 0;
+        int phase = TP_SHADE, who = -1, km = 0, mshape = -1;
+        double best = 0.0;
+        Ray ray;
+        V3 inv = dev::v3(0.0, 0.0, 0.0);
+        dev::Rng rng{0};
+        MemStack stk{nullptr, 0, 0, nullptr};
+        march::MarchState ms;
+        march::MarchStats mst{0, 0, 0, 0};
+        for (;;) {
+            const WfArgs &a = kargs(A);
+            const WfView &v = a.v;
+            if (!have) {
+                // the wave's lanes without a path take the next ones of the list (one atomic per wave)
+                const uint64_t need = __ballot(1);  // (the lanes still in the loop all need one here)
+                const int lead = __builtin_ctzll(need);
+                const uint32_t n = (uint32_t)__popcll(need);
+                uint32_t b = 0;
+                if ((int)lane_id() == lead) b = atomicAdd(&v.cnt[it * 4 + 3], n);
+                b = __shfl(b, lead, 64);
+                const uint32_t q = b + (uint32_t)__popcll(need & ((1ull << lane_id()) - 1ull));
+                if (q >= count) break;
+                uint32_t c;
+                load_path(v.in, v.list[q], &id, &ray, &rng.s, depth_it, &depth, &c, &who, &best);
+                stk = MemStack{v.ids + id, (size_t)v.cap, (int)c, EXT ? v.att + id : nullptr};
+                have = true;
+                phase = TP_SHADE;
+            }
+            if (phase == TP_TRACE) {
+                inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+                best = __builtin_inf();
+                who = -1;
+                // shaded at depth 0, only hit or miss matters (as the bounce kernel's `any`)
+                const bool any = depth == 0;
+                dev::closest_nomarch<false, EXT, BIGBVH>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+                km = 0;
+                phase = (any && who >= 0) || FK == march::F_NONE ? TP_SHADE : TP_SELECT;
+            }
+            if constexpr (FK != march::F_NONE) {  // (a scene without marched shapes never selects)
+            if (phase == TP_MARCH) {
+                const int st = march::march_step<false, true, FK>(ms, &mst);
+                if (st != march::M_RUNNING) {
+                    if (st == march::M_GUARD) dev::note_guard(a.sc.guard);
+                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
+                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
+                        best = ms.t;
+                        who = mshape;
+                    }
+                    phase = TP_SELECT;
+                }
+            }
+            if (phase == TP_SELECT) {
+                // next marched shape whose bound is entered before `best`
+                const dev::Scene &sc = a.sc;
+                phase = TP_SHADE;
+                while (km < sc.nmarch) {
+                    const int sh = sc.march[km++];
+                    const DBox &bx = sc.boxes[sh];
+                    if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
+                    const DShape &S = sc.shapes[sh];
+                    const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
+                    if (march::march_begin<FK>(dev::shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z,
+                                               &ms)) {
+                        mshape = sh;
+                        phase = TP_MARCH;
+                        break;
+                    }
+                }
+            }
+            }
+            if (phase == TP_SHADE) {
+                V3 leaf;
+                if (dev::shade<false, FK, EXT>(a.sc, who, best, ray, depth, stk, rng, a.P.s11, &leaf)) {
+                    end_path(v, id, stk, leaf);
+                    have = false;
+                } else {
+                    phase = TP_TRACE;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        uint32_t *cnt = kargs(A).v.cnt;
+        if (atomicAdd(&cnt[it * 4 + 2], 1u) == gridDim.x - 1) cnt[it * 4 + 0] = 0u;  // every block has read it
     }
 }
 
@@ -1145,6 +1299,21 @@ static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc,
     }
 }
 
+// The tail kernel's build for the scene (the bounce kernel's choice of march code and BVH walk).
+static void launch_tail(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it, int fkind,
+                        uint32_t max_paths) {
+    if (sc.ext)
+        wf_tail<march::F_ANY, true, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
+    else if (fkind != march::F_HEART)
+        wf_tail<march::F_ANY, false, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
+    else if (sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0)
+        wf_tail<march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it, max_paths);
+    else if (sc.nnodes >= BIG_BVH_NODES)
+        wf_tail<march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it, max_paths);
+    else
+        wf_tail<march::F_HEART, false, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
+}
+
 // Exactly the resident blocks of one kernel build (persistent grids).
 template <class K>
 static uint32_t resident_blocks(K kern) {
@@ -1313,14 +1482,19 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         if (want < march_blocks) march_blocks = want;
     }
     const uint32_t march_slice = (uint32_t)tu.wf_march_slice;
-    // Chunks run in rounds of `slots`, chunk j of a round on stream j, and are
-    // enqueued iteration by iteration across the round.  With wf_pingpong the
+    // the tail kernel's persistent grid: its resident blocks (a launch that finds too many live paths ends at once)
+    static const uint32_t tail_blocks = resident_blocks(wf_tail<march::F_HEART, false, false>);
+    const uint32_t tail_paths = (uint32_t)tu.wf_tail_paths;
+    // Chunk j of step k runs on stream j (its path-state slot); a step's chunks
+    // are enqueued iteration by iteration across the step.  With wf_pingpong the
     // bounce launches form one chain across the streams (each waits for the
     // previous one, in enqueue order), so one chunk's bounce (memory-bound)
     // runs beside the other chunk's compaction and march (VALU-bound) instead
     // of both chunks bouncing, then both marching, at the same time.
     struct Chunk {
         uint32_t g0, gt, s0, ns;
+        int slot;
+        uint32_t step;
     };
     // Sample chunks of a tile group: as few as fit ns samples each, rounded up
     // to whole rounds of `slots` (no round with an idle stream), with the
@@ -1329,25 +1503,63 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     uint32_t nchunks = (nsw + ns - 1) / ns;
     if (slots > 1 && nchunks > 1 && nchunks % (uint32_t)slots) nchunks += (uint32_t)slots - nchunks % (uint32_t)slots;
     if (nchunks > nsw) nchunks = nsw;
+    // Staggered streams (Tuning::wf_stagger): stream j > 0 starts with a chunk
+    // of j / slots of the samples and ends with one of (slots - j) / slots, so
+    // the streams run a chunk apart by 1 / slots of its length.  A chunk's last
+    // iterations are a few short, latency-bound launches (its march launches
+    // last as long as their slowest job whatever the queue length); streams in
+    // step reach those together and leave the device idle, staggered ones lay
+    // each tail beside another stream's full iterations.  The chunks of a
+    // group take consecutive sample ranges in the order they are expected to
+    // finish (which is the order of the per-pixel sums), so no reduce waits
+    // for a chunk that finishes later than its own.
+    const uint32_t S = (uint32_t)slots, R = nchunks / (S ? S : 1u);
+    const bool stagger = tu.wf_stagger && slots > 1 && nchunks % S == 0 && nsw / nchunks >= 2 * S;
     std::vector<Chunk> chunk_list;
+    uint32_t step0 = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        for (uint32_t c = 0, s0 = s_begin; c < nchunks; c++) {
-            const uint32_t n = nsw / nchunks + (c < nsw % nchunks ? 1u : 0u);  // <= ns
-            chunk_list.push_back(Chunk{g0, gt, s0, n});
-            s0 += n;
+        const size_t c0 = chunk_list.size();
+        std::vector<uint32_t> ticks;  // chunk sizes in 1/S of a chunk (stagger), or whole chunks
+        if (stagger) {
+            for (uint32_t k = 0; k <= R; k++) {
+                for (uint32_t j = 1; j < S; j++) {  // stream j: leading j/S, full chunks, trailing (S-j)/S
+                    chunk_list.push_back(Chunk{g0, gt, 0, 0, (int)j, step0 + k});
+                    ticks.push_back(k == 0 ? j : (k == R ? S - j : S));
+                }
+                if (k < R) {
+                    chunk_list.push_back(Chunk{g0, gt, 0, 0, 0, step0 + k});
+                    ticks.push_back(S);
+                }
+            }
+            step0 += R + 1;
+        } else {
+            for (uint32_t c = 0; c < nchunks; c++) {
+                chunk_list.push_back(Chunk{g0, gt, 0, 0, (int)(c % S), step0 + c / S});
+                ticks.push_back(1);
+            }
+            step0 += (nchunks + S - 1) / S;
+        }
+        uint64_t tot = 0, cum = 0;
+        for (uint32_t t : ticks) tot += t;
+        uint32_t s0 = s_begin;
+        for (size_t c = 0; c < ticks.size(); c++) {
+            cum += ticks[c];
+            const uint32_t s1 = s_begin + (uint32_t)((uint64_t)nsw * cum / tot);  // <= ceil(nsw / nchunks) <= ns each
+            chunk_list[c0 + c].s0 = s0;
+            chunk_list[c0 + c].ns = s1 - s0;
+            s0 = s1;
         }
     }
-    // The launches' argument blocks (WfArgs): chunk ci (on slot ci % slots) at iteration parity h is block
-    // 2 ci + h.  They are written to the pinned staging buffer, which the previous frame's copy must have read,
-    // and copied to the device on st after the previous frame's kernels (the wait on ws->done above), before
-    // the side streams fork.
+    // The launches' argument blocks (WfArgs): chunk ci at iteration parity h is block 2 ci + h.  They are
+    // written to the pinned staging buffer, which the previous frame's copy must have read, and copied to the
+    // device on st after the previous frame's kernels (the wait on ws->done above), before the side streams fork.
     const size_t nargs = chunk_list.size() * 2;
     if ((e = reserve_args(ws, nargs * sizeof(WfArgs))) != hipSuccess) return e;
     WfArgs *ah = (WfArgs *)ws->args_host, *ad = (WfArgs *)ws->args_dev;
     for (size_t ci = 0; ci < chunk_list.size(); ci++) {
         const Chunk &ch = chunk_list[ci];
-        const int j = (int)(ci % (size_t)slots);
+        const int j = ch.slot;
         WfView v = sl[j].v;
         v.tile0 = P0.tile_begin + ch.g0;
         v.npix = ch.gt * TILE * TILE;
@@ -1371,9 +1583,11 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // wf_pingpong bit 0: chain the bounce launches; bit 1: chain the march launches
     const bool pingpong = (tu.wf_pingpong & 1) && slots > 1, mchain = (tu.wf_pingpong & 2) && slots > 1;
     bool chained = false, mchained = false;  // ws->bev / ws->mev hold a launch to wait for
-    for (size_t r0 = 0; r0 < chunk_list.size(); r0 += (size_t)slots) {
-        const int nr = (int)(chunk_list.size() - r0 < (size_t)slots ? chunk_list.size() - r0 : (size_t)slots);
-        for (int j = 0; j < nr; j++) {  // the round's chunks: cleared counters
+    for (size_t r0 = 0; r0 < chunk_list.size();) {
+        size_t r1 = r0;  // the step's chunks [r0, r1), in sample order, at most one per stream
+        while (r1 < chunk_list.size() && chunk_list[r1].step == chunk_list[r0].step) r1++;
+        for (size_t c = r0; c < r1; c++) {  // the step's chunks: cleared counters
+            const int j = chunk_list[c].slot;
             const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
             if ((e = hipMemsetAsync(sl[j].v.cnt, 0, cnt_words * 4, cs)) != hipSuccess) return e;
             if (P0.stop) {
@@ -1382,15 +1596,22 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             }
         }
         for (int it = 0; it < iters; it++) {
-            for (int j = 0; j < nr; j++) {
+            for (size_t c = r0; c < r1; c++) {
+                const Chunk &ch = chunk_list[c];
+                const int j = ch.slot;
                 const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
-                const Chunk &ch = chunk_list[r0 + j];
-                const WfArgs *A = ad + 2 * (r0 + j) + (it & 1);
+                const WfArgs *A = ad + 2 * c + (it & 1);
                 const WfView &v = sl[j].v;
                 uint32_t *cp_blk = sl[j].cp_blk;
                 const uint32_t paths = ch.ns * ch.gt * TILE * TILE;
                 uint32_t bb = (paths + 255) / 256;
                 if (bb > WF_BOUNCE_CAP) bb = WF_BOUNCE_CAP;
+                if (tail_paths && it >= 1) {  // few live paths left: wf_tail runs them to their ends
+                    if ((e = timer_begin(ws->timer, cs, K_TAIL)) != hipSuccess) return e;
+                    launch_tail(tail_blocks, cs, sc, A, it, fkind, tail_paths);
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                }
                 if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
@@ -1410,11 +1631,12 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 const uint32_t ptiles = (paths + CP_TILE - 1) / CP_TILE;
                 const uint32_t *n_in = it == 0 ? nullptr : &v.cnt[it * 4 + 0];  // the bounce's input count
                 const CpLayout L = CpLayout::of(ptiles);
-                cp_count<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, n_in, paths);
-                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, L, &v.cnt[(it + 1) * 4 + 0], &v.cnt[it * 4 + 1],
-                                                &v.cnt[it * 4 + 2]);
-                cp_scatter<<<ptiles, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, &v.cnt[it * 4 + 2], v.list, v.mq, n_in,
-                                                        paths);
+                const uint32_t cgrid = CP_GRID && ptiles > CP_GRID ? CP_GRID : ptiles;
+                cp_count<<<cgrid, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, n_in, paths);
+                cp_scan<<<1, CP_BLOCK, 0, cs>>>(cp_blk, ptiles, L, n_in, paths, &v.cnt[(it + 1) * 4 + 0],
+                                                &v.cnt[it * 4 + 1], &v.cnt[it * 4 + 2]);
+                cp_scatter<<<cgrid, CP_BLOCK, 0, cs>>>(v.status, cp_blk, L, &v.cnt[it * 4 + 2], v.list, v.mq, n_in,
+                                                       paths);
                 if (P0.stop) stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, it);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
@@ -1435,13 +1657,14 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 }
             }
         }
-        // the per-pixel sums take the chunks in order
-        for (int j = 0; j < nr; j++) {
+        // the per-pixel sums take the chunks in sample order (chunk_list order)
+        for (size_t c = r0; c < r1; c++) {
+            const Chunk &ch = chunk_list[c];
+            const int j = ch.slot;
             const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
-            const Chunk &ch = chunk_list[r0 + j];
-            const WfArgs *A = ad + 2 * (r0 + j);
+            const WfArgs *A = ad + 2 * c;
             const uint32_t npix = ch.gt * TILE * TILE;
-            if (slots > 1 && r0 + j > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
+            if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
             // first: 1 = sums from zero, 2 = from out's running sums; last: 1 = means, 2 = running sums to out
             const int first = ch.s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
@@ -1454,6 +1677,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;
         }
+        r0 = r1;
     }
     // the caller's stream resumes after every side stream's last chunk
     for (int k = 0; k < slots - 1; k++) {

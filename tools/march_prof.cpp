@@ -4,6 +4,7 @@
 //                                                              build) and record every march start
 //   march_prof run <jobs.bin> [n]                               replay: counters, CPU time, and
 //                                                              exactness against a literal march
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -192,8 +193,10 @@ int main(int argc, char **argv) {
         std::vector<int> hist(64, 0);
         double hit_it = 0, miss_it = 0, hit_tries = 0, miss_tries = 0;
         long nh = 0, nm = 0;
+        std::vector<double> job_us(n);
         for (size_t i = 0; i < n; i++) {
             const Job &q = jobs[i];
+            const auto tj = std::chrono::steady_clock::now();
             march::MarchState m;
             march::march_begin(heartF(), q.step, q.passes, q.o[0], q.o[1], q.o[2], q.d[0], q.d[1], q.d[2], &m);
             unsigned long long it0 = g_prof.iters;
@@ -221,6 +224,7 @@ int main(int argc, char **argv) {
                     break;
                 }
             }
+            job_us[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tj).count() * 1e6;
             unsigned long long k = g_prof.iters - it0;
             hist[k < 63 ? k : 63]++;
             bool h = stt == march::M_DONE;
@@ -236,6 +240,14 @@ int main(int argc, char **argv) {
                (double)g_prof.iters / n, (double)ms.steps / n, (double)ms.tries / n, (double)ms.blocks / n,
                (double)g_prof.evals / n, (double)g_prof.lin_init / n, (double)g_prof.advance_loops / n,
                (double)g_prof.sir_inside / n, dt / n * 1e6);
+        {
+            std::vector<double> srt = job_us;
+            std::sort(srt.begin(), srt.end());
+            auto q = [&](double f) { return srt[std::min(n - 1, (size_t)(f * n))]; };
+            printf("job cpu us: p50 %.2f p90 %.2f p99 %.2f p99.9 %.2f p99.99 %.2f max %.2f (job %zu)\n", q(0.5), q(0.9),
+                   q(0.99), q(0.999), q(0.9999), srt[n - 1],
+                   (size_t)(std::max_element(job_us.begin(), job_us.end()) - job_us.begin()));
+        }
         printf("hit jobs: iters %.2f tries %.2f   miss jobs: iters %.2f tries %.2f\n", hit_it / nh, hit_tries / nh,
                miss_it / nm, miss_tries / nm);
         printf("advance literal adds per job %.2f\n", (double)g_prof.lit_adds / n);

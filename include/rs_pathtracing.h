@@ -166,7 +166,7 @@ int pt_renderer_peer_access(const pt_renderer *r, int *pairs, int *enabled);
  * the measured optimum): "engine" (0 auto, 1 megakernel,
  * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
  * "wf_bounce_waves", "wf_march_slice", "wf_march_blocks_per_cu",
- * "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "bvh_leaf" (shapes
+ * "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "wf_walk", "bvh_leaf" (shapes
  * per BVH leaf: setting it rebuilds the BVH on every device).  A new renderer
  * starts from the defaults; set_option changes them for every device of the
  * renderer (not while a render_start frame is in flight).  No knob changes the
@@ -335,11 +335,11 @@ int pt_render_stop_stats(pt_renderer *r, uint64_t *skipped, uint64_t *worked);
  * the summed HIP-event durations (ms) and launch counts per kernel kind since
  * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
  * reduce, [4] megakernel, [5] wavefront tail (wf_tail: a chunk's last live
- * paths run to their ends) — into ms[nkinds] / launches[nkinds] (either may be
+ * paths run to their ends), [6] BVH walk (wf_walk) — into ms[nkinds] / launches[nkinds] (either may be
  * NULL), then turns recording on (enable = 1) or off.  Events are recorded on
  * the stream each kernel is launched on.  PT_ERR_STATE while a render_start
  * frame is in flight (its band feeder records into the same timer). */
-#define PT_KERNEL_KINDS 6
+#define PT_KERNEL_KINDS 7
 int pt_kernel_timing(pt_renderer *r, int enable, double *ms, uint32_t *launches, size_t nkinds);
 
 /* Diagnostic of the wavefront kernels: returns (and clears) the counters

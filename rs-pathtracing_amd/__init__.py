@@ -498,7 +498,7 @@ def march_jobs(renderer: "HipRenderer", jobs, status=False):
     return (t, st, it) if status else (t, st == 1, it)
 
 
-KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", "tail"]
+KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", "tail", "walk"]
 
 
 def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
@@ -542,7 +542,7 @@ def option_names() -> list:
 OPTION_DEFAULTS = {"engine": 0, "mega_waves": 4, "diag": 0, "wf_slots": 2, "wf_paths": 3 << 24, "wf_min_chunks": 1,
                    "wf_bounce_waves": 3, "wf_march_slice": 256,
                    "wf_march_blocks_per_cu": 0, "wf_side_priority": 0,
-                   "wf_pingpong": 0, "wf_stagger": 0, "wf_tail_paths": 0, "bvh_leaf": 1}
+                   "wf_pingpong": 0, "wf_stagger": 0, "wf_tail_paths": 0, "wf_walk": 5, "bvh_leaf": 1}
 
 
 def shard_tiles(width: int, height: int, rank: int, world: int) -> int:

@@ -278,7 +278,7 @@ static dev::Scene dscene(const DeviceScene &s) {
 // ------------------------------------------------------------- tuning
 const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
                                     "wf_bounce_waves", "wf_march_slice",
-                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "bvh_leaf", nullptr};
+                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "wf_walk", "bvh_leaf", nullptr};
 
 static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
     struct F {
@@ -298,6 +298,7 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         {"wf_side_priority", &Tuning::wf_side_priority, -1, 1},
         {"wf_pingpong", &Tuning::wf_pingpong, 0, 3},
         {"wf_stagger", &Tuning::wf_stagger, 0, 1},
+        {"wf_walk", &Tuning::wf_walk, 0, 8},
         {"bvh_leaf", &Tuning::bvh_leaf, 1, 16},
     };
     *iv = nullptr;
@@ -330,6 +331,7 @@ int tuning_set(Tuning *t, const char *name, int64_t v) {
     if (v < lo || v > hi) return PT_ERR_INVALID;
     if (!strcmp(name, "wf_bounce_waves") && !(v == 2 || v == 3 || v == 4 || v == 5 || v == 6 || v == 8))
         return PT_ERR_INVALID;
+    if (!strcmp(name, "wf_walk") && !(v == 0 || v == 4 || v == 5 || v == 6 || v == 8)) return PT_ERR_INVALID;
     if (lv) *lv = v;
     else *iv = (int)v;
     return PT_OK;

@@ -29,7 +29,7 @@ struct DeviceScene {
 // reused by every frame of a renderer.
 // Per-kernel launch timing (pt_kernel_timing): HIP events recorded on the
 // launch stream around every render-path kernel while enabled.
-enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_TAIL = 5, K_KINDS = 6 };
+enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_TAIL = 5, K_WALK = 6, K_KINDS = 7 };
 struct KernelTimer;
 KernelTimer *timer_new();
 void timer_free(KernelTimer *t);
@@ -53,6 +53,8 @@ struct Tuning {
     int wf_side_priority = 0;        // the library's chunk streams' priority (-1 low, 0 normal, 1 high)
     int wf_pingpong = 0;             // bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
     int wf_stagger = 0;              // 1: chunk streams offset by 1/slots of a chunk (staggered sample chunks; C2 -1.2 %, depth 50 -3 %)
+    int wf_walk = 5;                 // large-tree scenes without marched shapes: the BVH walk in its own kernel (wf_walk)
+                                     // at this register budget, waves per SIMD (4, 5, 6, 8; 0: the walk in the bounce)
     int64_t wf_tail_paths = 0;       // a chunk's live paths from which wf_tail runs them to their ends (0 = never)
     int bvh_leaf = 1;                // shapes per BVH leaf (1..16; C5 677 / 609 / 534 M samples/s at 1 / 2 / 4)
 };

@@ -318,7 +318,9 @@ constexpr int WF_PREDICT = 4;
 // full s_waitcnt so the memory waits it causes are charged to it (tuning
 // only): list load, state loads, shade, unwind, trace, march pre-check,
 // stores; summed into diag[36..42].
-template <int NW, bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false, bool BIGBVH = false>
+// SPLIT (the large-tree builds without marched shapes, C5): the kernel only shades and stores the new ray; wf_walk
+// traces it after the compaction (PT_WF_WALK).
+template <int NW, bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false, bool BIGBVH = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict__ A, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -406,7 +408,10 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
                 }
             }
         }
-        if (live) {
+        if (live && SPLIT) {  // the ray is traced by wf_walk (pending hit: none yet)
+            best = __builtin_inf();
+            who = -1;
+        } else if (live) {
             PT_LP(TRACE);
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             best = __builtin_inf();
@@ -952,6 +957,41 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
     }
 }
 
+// The BVH walk of the large-tree scenes without marched shapes (C5) as its own
+// kernel (PT_WF_WALK, round 5): the walk is latency-bound (a chain of
+// dependent node loads per lane, ~70 % of the bounce's wave cycles waiting on
+// memory), and inside the bounce kernel its lanes run at the bounce's register
+// budget (118 VGPRs: 4 waves per SIMD).  Alone it needs far fewer registers,
+// so more waves -- more independent node chains -- are in flight per SIMD.
+// It runs after the compaction of iteration it, over the live list of it + 1:
+// the ray each bounce stored, traced through the uniform list and the BVH
+// (closest_nomarch, the same code and tie rule as the bounce's trace), and
+// (best, who) written back in place; the next bounce shades them.
+template <int WAVES>
+__global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__ A, int it) {
+    const uint32_t count = kargs(A).v.cnt[(it + 1) * 4 + 0];
+    const uint32_t stride = gridDim.x * blockDim.x;
+    // the trace after bounce it is shaded at depth P.depth - it: at 0 only hit or miss matters
+    const bool any = kargs(A).P.depth == (uint32_t)it;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const WfArgs &a = kargs(A);
+        const WfView &v = a.v;
+        const uint32_t p = v.list[i];
+        const double *d = v.out.d8(p);
+        constexpr uint32_t B = PathSoA::BLK;
+        Ray ray;
+        ray.o = dev::v3(d[PathSoA::OX * B], d[PathSoA::OY * B], d[PathSoA::OZ * B]);
+        ray.d = dev::v3(d[PathSoA::DX * B], d[PathSoA::DY * B], d[PathSoA::DZ * B]);
+        const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+        double best = __builtin_inf();
+        int who = -1;
+        dev::closest_nomarch<false, false, true>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+        v.out.t(p) = best;
+        uint32_t &w = v.out.who(p);
+        w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;
+    }
+}
+
 // The tail of a chunk (round 5).  The live paths of a chunk decay by ~10 %
 // per bounce; once few are left, each iteration's launches are latency-bound:
 // a persistent march launch lasts as long as its slowest job (~200-250 us at
@@ -1258,9 +1298,22 @@ static hipError_t reserve(WaveWorkspace *ws, size_t bytes) {
 
 // BVH nodes per octant layout from which the bounce runs its FMA_SLAB build
 // (dev::closest_nomarch): C5's 100k-sphere tree has ~200k, cornell's ~960.
+// The scenes whose BVH walk runs in wf_walk (Tuning::wf_walk): a large tree and no marched shape (C5).
+static bool walk_split(const dev::Scene &sc, const Tuning &tu) {
+    return tu.wf_walk && !sc.ext && sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0;
+}
+
 template <int NW, bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it,
-                          unsigned long long *diag, int fkind, int waves) {
+                          unsigned long long *diag, int fkind, int waves, bool split) {
+    if (split) {  // shade and store the new ray only: wf_walk traces it
+        switch (waves) {
+        case 4: wf_bounce<NW, FIRST, 4, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 5: wf_bounce<NW, FIRST, 5, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        default: wf_bounce<NW, FIRST, 3, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        }
+        return;
+    }
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
         wf_bounce<NW, FIRST, 2, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
         return;
@@ -1485,6 +1538,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     // the tail kernel's persistent grid: its resident blocks (a launch that finds too many live paths ends at once)
     static const uint32_t tail_blocks = resident_blocks(wf_tail<march::F_HEART, false, false>);
     const uint32_t tail_paths = (uint32_t)tu.wf_tail_paths;
+    const bool split = walk_split(sc, tu);
     // Chunk j of step k runs on stream j (its path-state slot); a step's chunks
     // are enqueued iteration by iteration across the step.  With wf_pingpong the
     // bounce launches form one chain across the streams (each waits for the
@@ -1616,9 +1670,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
                 if (it == 0)
-                    launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves);
+                    launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves,
+                                            split);
                 else
-                    launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves);
+                    launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves, split);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (pingpong) {
@@ -1640,6 +1695,17 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if (P0.stop) stop_gate<<<1, 64, 0, cs>>>(P0.stop, v.cnt, it);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                if (split) {  // the new rays' BVH walk, over the live list of it + 1
+                    if ((e = timer_begin(ws->timer, cs, K_WALK)) != hipSuccess) return e;
+                    switch (tu.wf_walk) {  // the walk's register budget, waves per SIMD
+                    case 4: wf_walk<4><<<bb, 256, 0, cs>>>(A, it); break;
+                    case 6: wf_walk<6><<<bb, 256, 0, cs>>>(A, it); break;
+                    case 8: wf_walk<8><<<bb, 256, 0, cs>>>(A, it); break;
+                    default: wf_walk<5><<<bb, 256, 0, cs>>>(A, it); break;
+                    }
+                    if ((e = hipGetLastError()) != hipSuccess) return e;
+                    if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
+                }
                 if (sc.nmarch == 0) continue;  // no ray-marched shape: the march queue is always empty
                 if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;

@@ -106,6 +106,13 @@ def test_c5_synthetic_100k_spheres(pt, c5):
     assert img.mean() > 0.05
     r.set_option("bvh_leaf", 3)  # the BVH rebuilt with 3 shapes per leaf: the same closest hits
     assert np.array_equal(r.render(cam, pt.ImageParams(160, 90), 2, seed=2), ref)
+    r.set_option("bvh_leaf", 1)
+    # the wavefront engine (this frame is below its automatic threshold), with the BVH walk in the bounce kernel
+    # (wf_walk 0) and in its own kernel at each register budget
+    r.set_option("engine", 2)
+    for walk in (0, 4, 5, 6, 8):
+        r.set_option("wf_walk", walk)
+        assert np.array_equal(r.render(cam, pt.ImageParams(160, 90), 2, seed=2), ref), walk
 
 
 def test_shard_pixels_matches_device_deal(pt, cornell):

@@ -69,6 +69,8 @@ FLOP_WEIGHTS = {
     "lambert": 20, "metal": 25, "dielectric": 40, "reject_tries": 14, "unwind": 3,
 }
 MARCH_EVENTS = ("test_march", "march_slabs", "march_steps", "march_tries", "march_blocks")
+# the trace's events: in the bounce kernel, or in wf_walk for the large-tree scenes without marched shapes
+WALK_EVENTS = ("test_sphere", "test_rect", "test_cube", "node_slabs")
 
 
 def f32_node_flops_per_sample(counts):
@@ -80,6 +82,11 @@ def f32_node_flops_per_sample(counts):
 
 def kt_src_has_bounce(src):
     return src.get("bounce", (0, 0))[1] > 0
+
+
+def node_kernel(src):
+    """The kernel kind that tests the BVH nodes: wf_walk when it ran, else the bounce kernel."""
+    return "walk" if src.get("walk", (0, 0))[1] > 0 else "bounce"
 
 
 def flops_per_sample(cnt, keys=None):
@@ -481,8 +488,13 @@ def main():
         if multi:  # kernel timing covers the first device: its tile share
             share = pt.shard_tiles(W, H, 0, args.gpus) / pt.shard_tiles(W, H, 0, 1)
         samples_share = samples_frame * share
+        src = kt_iso if kt_iso is not None else kt
+        nfr = 1 if kt_iso is not None else args.steps
+        walked = node_kernel(src) == "walk"  # the trace runs in wf_walk (large tree, no marched shape)
+        bounce_ev = [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS and not (walked and k in WALK_EVENTS)]
         f_weights = {"march": flops_per_sample(counts, MARCH_EVENTS),
-                     "bounce": flops_per_sample(counts, [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS]),
+                     "bounce": flops_per_sample(counts, bounce_ev),
+                     "walk": flops_per_sample(counts, WALK_EVENTS) if walked else 0.0,
                      "megakernel": F}
         workload = "%s %dx%d %dspp depth %d" % (args.scene, W, H, spp, args.depth)
         # algorithmic FLOPs per sample: from the f64 instruction counters of a committed PMC pass of this
@@ -493,16 +505,14 @@ def main():
         if fl:
             for k, v in fl["kinds"].items():
                 f_kind[k] = v["algorithmic_flops_per_sample"]
-            F = f_kind["bounce"] + f_kind["march"]
-        kname = {"bounce": "wf_bounce", "march": "wf_march", "megakernel": "render_tiles"}
-        src = kt_iso if kt_iso is not None else kt
-        nfr = 1 if kt_iso is not None else args.steps
-        dom = max(("bounce", "march", "megakernel"), key=lambda k: src[k][0])
+            F = f_kind["bounce"] + f_kind["march"] + f_kind.get("walk", 0.0)
+        kname = {"bounce": "wf_bounce", "march": "wf_march", "walk": "wf_walk", "megakernel": "render_tiles"}
+        dom = max(("bounce", "march", "walk", "megakernel"), key=lambda k: src.get(k, (0, 0))[0])
         dom_ms, dom_n = src[dom]
         achieved = f_kind[dom] * samples_share * nfr / (dom_ms / 1e3) / 1e12
         per_kernel = {}
-        for k in ("bounce", "march", "megakernel"):
-            ms_k, n_k = src[k]
+        for k in ("bounce", "march", "walk", "megakernel"):
+            ms_k, n_k = src.get(k, (0.0, 0))
             if n_k:
                 a_k = f_kind[k] * samples_share * nfr / (ms_k / 1e3) / 1e12
                 per_kernel[kname[k]] = {"achieved": round(a_k, 4), "frac": round(a_k / FP64_PEAK_TFLOPS, 5),
@@ -513,17 +523,18 @@ def main():
         # the large-tree bounce build tests BVH nodes in f32: 6 FMAs per node slab, outside the f64
         # counters; reported beside the f64 roofline, and both shares of the VALU's FLOP rate summed
         f32_kind = {}
-        if r.get_option("bvh_nodes") >= BIG_BVH_NODES and kt_src_has_bounce(src):
+        nk = node_kernel(src)
+        if r.get_option("bvh_nodes") >= BIG_BVH_NODES and src.get(nk, (0, 0))[1] > 0:
             f32_ps = f32_node_flops_per_sample(counts)
-            ms_b, _ = src["bounce"]
+            ms_b, _ = src[nk]
             a32 = f32_ps * samples_share * nfr / (ms_b / 1e3) / 1e12
-            f32_kind = {"kernel": "wf_bounce", "flops_per_sample": round(f32_ps, 1), "achieved": round(a32, 4),
+            f32_kind = {"kernel": kname[nk], "flops_per_sample": round(f32_ps, 1), "achieved": round(a32, 4),
                         "peak": FP32_PEAK_TFLOPS, "frac": round(a32 / FP32_PEAK_TFLOPS, 5),
                         "source": "(node_slabs - bounces) events (pt_count_work) x 12: six f32 FMAs per node, "
                                   "less the root test the large-tree walk skips once per trace"}
-            if "wf_bounce" in per_kernel:
-                per_kernel["wf_bounce"]["valu_frac_f64_plus_f32"] = round(
-                    per_kernel["wf_bounce"]["frac"] + a32 / FP32_PEAK_TFLOPS, 5)
+            if kname[nk] in per_kernel:
+                per_kernel[kname[nk]]["valu_frac_f64_plus_f32"] = round(
+                    per_kernel[kname[nk]]["frac"] + a32 / FP32_PEAK_TFLOPS, 5)
         out_bytes = 24.0 * W * H * share
         tuning = {k: v for k, v in r.options().items() if v != pt.OPTION_DEFAULTS.get(k)}
         rec = {
@@ -551,8 +562,9 @@ def main():
                          "flops_source": ("f64 instruction counters x mean active lanes, %s (%s; scripts/pmc_flops.py); "
                                           "event weights give %.1f FLOP/sample (%.2fx)"
                                           % (ff.relative_to(ROOT), fl["workload"],
-                                             f_weights["bounce"] + f_weights["march"],
-                                             (f_weights["bounce"] + f_weights["march"]) / F) if fl else
+                                             f_weights["bounce"] + f_weights["march"] + f_weights["walk"],
+                                             (f_weights["bounce"] + f_weights["march"] + f_weights["walk"]) / F)
+                                          if fl else
                                           "kernel event counters (pt_count_work) x FLOP_WEIGHTS (%s)" % f_why),
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},

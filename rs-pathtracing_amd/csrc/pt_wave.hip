@@ -967,28 +967,65 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // the ray each bounce stored, traced through the uniform list and the BVH
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
+#ifndef PT_WALK_OCT
+#define PT_WALK_OCT 1  // a block's 256 rays regrouped by direction octant before the walk (0: in list order)
+#endif
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__ A, int it) {
+    __shared__ uint32_t pos[256];      // the block's list positions, grouped by octant
+    __shared__ uint32_t wcount[4][9];  // rays per (wave, octant; 8: none)
     const uint32_t count = kargs(A).v.cnt[(it + 1) * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     // the trace after bounce it is shaded at depth P.depth - it: at 0 only hit or miss matters
     const bool any = kargs(A).P.depth == (uint32_t)it;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {  // (block-uniform)
         const WfArgs &a = kargs(A);
         const WfView &v = a.v;
-        const uint32_t p = v.list[i];
-        const double *d = v.out.d8(p);
+        const uint32_t i = base + threadIdx.x;
         constexpr uint32_t B = PathSoA::BLK;
-        Ray ray;
-        ray.o = dev::v3(d[PathSoA::OX * B], d[PathSoA::OY * B], d[PathSoA::OZ * B]);
-        ray.d = dev::v3(d[PathSoA::DX * B], d[PathSoA::DY * B], d[PathSoA::DZ * B]);
-        const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-        double best = __builtin_inf();
-        int who = -1;
-        dev::closest_nomarch<false, false, true>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
-        v.out.t(p) = best;
-        uint32_t &w = v.out.who(p);
-        w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;
+        uint32_t p;
+        if (PT_WALK_OCT) {
+            // Counting sort of the block's rays by the octant of their direction (the BVH layout they walk),
+            // stable, so each group keeps the list's pixel order: a wave then walks one or two layouts with
+            // neighbouring origins instead of up to eight (the rays after a diffuse bounce spread over the
+            // hemisphere's octants).
+            const uint32_t q = i < count ? v.list[i] : 0u;
+            const double *d = v.out.d8(q);
+            const uint32_t oct = i < count ? (__builtin_signbit(d[PathSoA::DX * B]) ? 1u : 0u) |
+                                                 (__builtin_signbit(d[PathSoA::DY * B]) ? 2u : 0u) |
+                                                 (__builtin_signbit(d[PathSoA::DZ * B]) ? 4u : 0u)
+                                           : 8u;
+            const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+            uint32_t rank = 0;
+            for (uint32_t o = 0; o < 9; o++) {
+                const uint64_t m = __ballot(oct == o);
+                if (oct == o) rank = (uint32_t)__popcll(m & ((1ull << ln) - 1ull));
+                if (ln == 0) wcount[wv][o] = (uint32_t)__popcll(m);
+            }
+            __syncthreads();
+            uint32_t at = 0;  // rays of lower octants in the block, then of this octant in earlier waves
+            for (uint32_t o = 0; o < 9; o++)
+                for (uint32_t w2 = 0; w2 < 4; w2++) at += (o < oct || (o == oct && w2 < wv)) ? wcount[w2][o] : 0u;
+            pos[at + rank] = q;
+            __syncthreads();
+            p = pos[threadIdx.x];
+            __syncthreads();  // (pos and wcount are rewritten by the next trip)
+        } else {
+            p = i < count ? v.list[i] : 0u;
+        }
+        if (i < count) {  // (the block's first count - base positions hold its rays)
+            const double *d = v.out.d8(p);
+            Ray ray;
+            ray.o = dev::v3(d[PathSoA::OX * B], d[PathSoA::OY * B], d[PathSoA::OZ * B]);
+            ray.d = dev::v3(d[PathSoA::DX * B], d[PathSoA::DY * B], d[PathSoA::DZ * B]);
+            const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+            double best = __builtin_inf();
+            int who = -1;
+            dev::closest_nomarch<false, false, true>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+            v.out.t(p) = best;
+            uint32_t &w = v.out.who(p);
+            w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;
+        }
     }
 }
 

@@ -44,7 +44,8 @@ acc = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         name = row["Kernel_Name"]
-        kind = "bounce" if "wf_bounce" in name else "march" if "wf_march" in name else None
+        kind = ("bounce" if "wf_bounce" in name else "march" if "wf_march" in name else
+                "walk" if "wf_walk" in name else None)
         if kind:
             acc[kind][row["Counter_Name"]] += float(row["Counter_Value"])
 res = {"workload": workload, "source_id": source_id(), "frames": frames, "samples_per_frame": samples,

@@ -25,7 +25,7 @@ def source_id():
     import __graft_entry__
     return __graft_entry__.load_package().source_id()
 
-KINDS = {"pt::wf_bounce<": "bounce", "pt::wf_march<": "march", "pt::render_tiles": "megakernel"}
+KINDS = {"pt::wf_bounce<": "bounce", "pt::wf_march<": "march", "pt::wf_walk<": "walk", "pt::render_tiles": "megakernel"}
 
 
 def kind_of(name):

@@ -295,7 +295,10 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 
 // points along a march job's chord whose sign of f predicts a hit (queue
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
-constexpr int WF_PREDICT = 4;
+#ifndef PT_WF_PREDICT
+#define PT_WF_PREDICT 4
+#endif
+constexpr int WF_PREDICT = PT_WF_PREDICT;
 
 #ifndef PT_MARCH_SPREAD
 #define PT_MARCH_SPREAD 1  // a short march queue dealt in runs of count / blocks (1), or always in slice runs (0)
@@ -968,12 +971,14 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
 #ifndef PT_WALK_OCT
-#define PT_WALK_OCT 1  // a block's 256 rays regrouped by direction octant before the walk (0: in list order)
+#define PT_WALK_OCT 1  // a block's 256 rays regrouped by direction octant before the walk (0: in list order;
+                       // 2: by octant and major axis)
 #endif
 template <int WAVES>
 __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__ A, int it) {
     __shared__ uint32_t pos[256];      // the block's list positions, grouped by octant
-    __shared__ uint32_t wcount[4][9];  // rays per (wave, octant; 8: none)
+    constexpr uint32_t NB = PT_WALK_OCT == 2 ? 25u : 9u;  // groups (the last: no ray)
+    __shared__ uint32_t wcount[4][NB];  // rays per (wave, group)
     const uint32_t count = kargs(A).v.cnt[(it + 1) * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     // the trace after bounce it is shaded at depth P.depth - it: at 0 only hit or miss matters
@@ -991,20 +996,24 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
             // hemisphere's octants).
             const uint32_t q = i < count ? v.list[i] : 0u;
             const double *d = v.out.d8(q);
-            const uint32_t oct = i < count ? (__builtin_signbit(d[PathSoA::DX * B]) ? 1u : 0u) |
-                                                 (__builtin_signbit(d[PathSoA::DY * B]) ? 2u : 0u) |
-                                                 (__builtin_signbit(d[PathSoA::DZ * B]) ? 4u : 0u)
-                                           : 8u;
+            const double dx = d[PathSoA::DX * B], dy = d[PathSoA::DY * B], dz = d[PathSoA::DZ * B];
+            uint32_t oct = (__builtin_signbit(dx) ? 1u : 0u) | (__builtin_signbit(dy) ? 2u : 0u) |
+                           (__builtin_signbit(dz) ? 4u : 0u);
+            if (PT_WALK_OCT == 2) {  // and the direction's major axis
+                const double ax = fabs(dx), ay = fabs(dy), az = fabs(dz);
+                oct = oct * 3u + (ax >= ay && ax >= az ? 0u : (ay >= az ? 1u : 2u));
+            }
+            if (i >= count) oct = NB - 1u;
             const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
             uint32_t rank = 0;
-            for (uint32_t o = 0; o < 9; o++) {
+            for (uint32_t o = 0; o < NB; o++) {
                 const uint64_t m = __ballot(oct == o);
                 if (oct == o) rank = (uint32_t)__popcll(m & ((1ull << ln) - 1ull));
                 if (ln == 0) wcount[wv][o] = (uint32_t)__popcll(m);
             }
             __syncthreads();
-            uint32_t at = 0;  // rays of lower octants in the block, then of this octant in earlier waves
-            for (uint32_t o = 0; o < 9; o++)
+            uint32_t at = 0;  // rays of lower groups in the block, then of this group in earlier waves
+            for (uint32_t o = 0; o < NB; o++)
                 for (uint32_t w2 = 0; w2 < 4; w2++) at += (o < oct || (o == oct && w2 < wv)) ? wcount[w2][o] : 0u;
             pos[at + rank] = q;
             __syncthreads();

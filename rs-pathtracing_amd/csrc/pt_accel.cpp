@@ -205,6 +205,71 @@ struct Builder {
 
 }  // namespace
 
+// The quantized nodes of a large tree (DNodeQ): per axis the grid step is the smallest power of two with which
+// 65535 steps from g0 = floor(lo / step) * step cover the root box; every lo plane is rounded down to the grid
+// and every hi plane up, checked in f64 (g0 + q * step is exact there).  Left empty if a leaf's skip is not the
+// next node (the threaded layouts always make it so) or a link does not fit.
+void build_qnodes(Accel &a) {
+    const size_t per_oct = a.nodes.size() / BVH_OCTANTS;
+    double lo[3], hi[3];
+    for (int k = 0; k < 3; k++) lo[k] = INFINITY, hi[k] = -INFINITY;
+    for (const DNode &n : a.nodes)
+        for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], n.lo[k]), hi[k] = std::max(hi[k], n.hi[k]);
+    for (int k = 0; k < 3; k++) {
+        if (!(std::isfinite(lo[k]) && std::isfinite(hi[k]))) return;
+        double step = std::ldexp(1.0, std::ilogb(std::max(hi[k] - lo[k], 1e-300) / 65535.0));
+        for (;;) {
+            const double g0 = std::floor(lo[k] / step) * step;
+            if (std::ceil((hi[k] - g0) / step) <= 65535.0 && g0 <= lo[k]) {
+                a.qg0[k] = g0;
+                a.qgs[k] = step;
+                break;
+            }
+            step *= 2.0;
+        }
+    }
+    auto q_down = [&](double v, int k) {
+        double q = std::floor((v - a.qg0[k]) / a.qgs[k]);
+        while (q > 0 && a.qg0[k] + q * a.qgs[k] > v) q -= 1.0;
+        return std::max(0.0, std::min(65535.0, q));
+    };
+    auto q_up = [&](double v, int k) {
+        double q = std::ceil((v - a.qg0[k]) / a.qgs[k]);
+        while (q < 65535.0 && a.qg0[k] + q * a.qgs[k] < v) q += 1.0;
+        return std::max(0.0, std::min(65535.0, q));
+    };
+    std::vector<DNodeQ> out;
+    out.reserve(a.nodes.size());
+    double bound = 0.0;
+    for (int k = 0; k < 3; k++) bound = std::max(bound, std::fabs(a.qg0[k]));
+    for (size_t ni = 0; ni < a.nodes.size(); ni++) {
+        const DNode &n = a.nodes[ni];
+        const int oct = (int)(ni / per_oct);
+        DNodeQ c{};
+        for (int k = 0; k < 3; k++) {
+            const double ql = q_down(n.lo[k], k), qh = q_up(n.hi[k], k);
+            if (a.qg0[k] + ql * a.qgs[k] > n.lo[k] || a.qg0[k] + qh * a.qgs[k] < n.hi[k]) return;  // (cannot happen)
+            bound = std::max({bound, std::fabs(a.qg0[k] + ql * a.qgs[k]), std::fabs(a.qg0[k] + qh * a.qgs[k])});
+            const bool neg = (oct >> k) & 1;  // the octant's rays move toward -k: hi is the near plane
+            c.q[k] = (uint16_t)(neg ? qh : ql);
+            c.q[3 + k] = (uint16_t)(neg ? ql : qh);
+        }
+        if (n.count == 0) {
+            if (n.skip < 0) return;
+            c.link = (uint32_t)n.skip;
+        } else {
+            if ((size_t)n.skip != ni % per_oct + 1 || n.count > 63) return;
+            const uint32_t fc = a.cnodes[ni].first_count;  // the compact form's leaf: direct id or list index
+            const bool direct = fc >> 31;
+            c.link = 1u << 31 | (direct ? 1u << 30 : 0u) | (uint32_t)n.count << 24 | (fc & 0xffffffu);
+        }
+        out.push_back(c);
+    }
+    a.qnodes.swap(out);
+    a.qbound = (float)bound;
+    if ((double)a.qbound < bound) a.qbound = std::nextafter(a.qbound, INFINITY);
+}
+
 Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
     Accel a;
     a.boxes.reserve(sc.shapes.size());
@@ -273,6 +338,7 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
             c.first_count = (uint32_t)n.first | (uint32_t)n.count << 24;
         a.cnodes.push_back(c);
     }
+    if (per_oct >= (size_t)BIG_BVH_NODES) build_qnodes(a);
     return a;
 }
 

@@ -38,12 +38,19 @@ struct Accel {
     std::vector<int32_t> march;  // ray-marched shapes
     std::vector<DBox> boxes;     // padded world AABB per shape
     float bvh_bound = 0.f;  // >= |every plane of cnodes| (dev::Scene::bvh_bound)
+    // the quantized nodes (trees of at least BIG_BVH_NODES nodes per layout; empty otherwise) and their grid
+    std::vector<DNodeQ> qnodes;
+    double qg0[3] = {0, 0, 0}, qgs[3] = {0, 0, 0};
+    float qbound = 0.f;  // >= |every quantized plane| and >= |qg0|
 };
 
 constexpr int LIN_MAX = 32;  // JSON shape count up to which the JSON shapes form `lin`
 
 // leaf_max: shapes per BVH leaf (the renderer option "bvh_leaf")
 Accel build_accel(const Scene &sc, int json_shapes, int leaf_max = 1);
+// the quantized nodes of a's layouts (build_accel does this for trees of at least BIG_BVH_NODES nodes per layout;
+// tests call it for smaller ones)
+void build_qnodes(Accel &a);
 // conservative world AABB of one shape (reference get_bounding_box + padding)
 DBox shape_box(const HostShape &s);
 

@@ -290,8 +290,8 @@ void free_share(GpuShare &g) {
     (void)hipSetDevice(g.device);
     if (g.stream) (void)hipStreamSynchronize(g.stream);
     DeviceScene &d = g.ds;
-    void *bufs[] = {d.shapes, d.mats, d.nodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images, d.pixels,
-                    d.guard};
+    void *bufs[] = {d.shapes, d.mats, d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images,
+                    d.pixels, d.guard};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     d = DeviceScene{};
@@ -313,6 +313,7 @@ void free_share(GpuShare &g) {
 // structure.
 struct StagedAccel {
     DNodeC *nodes = nullptr;
+    DQGrid *qnodes = nullptr;
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     int nnodes = 0, nlin = 0, nmarch = 0;
@@ -326,7 +327,7 @@ struct StagedAccel {
 
 void free_staged(int device, StagedAccel &a) {
     (void)hipSetDevice(device);
-    void *bufs[] = {a.nodes, a.leaf, a.lin, a.march, a.boxes};
+    void *bufs[] = {a.nodes, a.qnodes, a.leaf, a.lin, a.march, a.boxes};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     a = StagedAccel{};
@@ -348,6 +349,16 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out, int *fault = nul
     upload(&a.lin, acc.lin);
     upload(&a.march, acc.march);
     upload(&a.boxes, acc.boxes);
+    if (err == hipSuccess && !acc.qnodes.empty()) {  // the grid, then the quantized layouts
+        DQGrid g{};
+        for (int k = 0; k < 3; k++) g.g0[k] = acc.qg0[k], g.gs[k] = acc.qgs[k];
+        g.bound = acc.qbound;
+        const size_t nb = acc.qnodes.size() * sizeof(DNodeQ);
+        if (fault && *fault > 0 && (*fault)-- == 1) err = hipErrorOutOfMemory;
+        if (err == hipSuccess) err = hipMalloc((void **)&a.qnodes, sizeof(DQGrid) + nb);
+        if (err == hipSuccess) err = hipMemcpy(a.qnodes, &g, sizeof g, hipMemcpyHostToDevice);
+        if (err == hipSuccess) err = hipMemcpy(a.qnodes + 1, acc.qnodes.data(), nb, hipMemcpyHostToDevice);
+    }
     if (err != hipSuccess) {
         free_staged(device, a);
         return hip_fail(err, "uploading the acceleration structure");
@@ -366,8 +377,9 @@ int commit_accel(GpuShare &g, StagedAccel &a) {
     HIP_TRY(hipSetDevice(g.device));
     HIP_TRY(hipDeviceSynchronize());
     DeviceScene &d = g.ds;
-    StagedAccel old{d.nodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.bvh_bound};
+    StagedAccel old{d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.bvh_bound};
     d.nodes = a.nodes;
+    d.qnodes = a.qnodes;
     d.leaf = a.leaf;
     d.lin = a.lin;
     d.march = a.march;

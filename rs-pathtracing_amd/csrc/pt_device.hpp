@@ -343,6 +343,7 @@ struct Scene {
     const DShape *__restrict__ shapes;
     const DMaterial *__restrict__ mats;
     const DNodeC *__restrict__ nodes;  // compact form (pt_types.hpp)
+    const DQGrid *__restrict__ qnodes;  // quantized form after its grid (large trees; else null)
     const int32_t *__restrict__ leaf;
     const int32_t *__restrict__ lin;
     const int32_t *__restrict__ march;
@@ -411,7 +412,10 @@ PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first,
     }
 }
 
-template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false>
+// QN (with FMA_SLAB and PT_SLAB32; sc.qnodes set): the BVH walk reads the quantized nodes (DNodeQ), 16 bytes
+// instead of 32: t = fma(q, gs / d, (g0 - o) / d -/+ e') per plane, the same culling with the grid folded into
+// the per-ray offsets and a wider margin (below).
+template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false, bool QN = false>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
                            Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
@@ -476,6 +480,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // below 1e-30, where an f32 flush of b * 1/d could exceed the widening; min_t is rounded down and best up.
     // The hits are decided by the exact f64 leaf tests as in every walk.
     constexpr bool S32 = FMA_SLAB && PT_SLAB32;
+    constexpr bool Q = S32 && QN;
     auto axis32 = [&](double o, double iv, float *i32, float *lo32, float *hi32) {
         const double m = -(o * iv);
         const bool fits = fabs(iv) < 1e30 && fabs(iv) > 1e-30 && fabs(m) < 1e30;
@@ -484,8 +489,29 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
         *lo32 = fits ? (float)(m - e) : __builtin_nanf("");
         *hi32 = fits ? (float)(m + e) : __builtin_nanf("");
     };
+    // QN: plane b = g0 + q gs (exact), so t = (b - o) / d = q (gs / d) + (g0 / d - o / d).  With i32 = fl32(1/d),
+    // si = gs * i32 (exact: gs is a power of two; |si| > 1e-30 is required, so no f32 flush), gl = fl32(g0 * i32
+    // + (m -/+ e')) and the fma's one rounding, the computed t is off the widened real t by at most
+    // 2^-24 (3B + 2|o|) |1/d| + 2^-23 e' (B >= |b|, |g0|: DQGrid::bound), far inside e' = 2^-19 (B + |o|) |1/d|:
+    // the culling stays conservative.  An axis whose values do not fit f32 is left open (NaN t's), as above.
+    auto axisq = [&](int k, double o, double iv, float *si, float *gln, float *glf) {
+        const double m = -(o * iv);
+        const float i32 = (float)iv;
+        const double s64 = (double)i32 * sc.qnodes->gs[k];
+        const double e = 0x1p-19 * ((double)sc.qnodes->bound + fabs(o)) * fabs(iv) + 1e-30;
+        const double g = sc.qnodes->g0[k] * (double)i32;
+        const bool fits = fabs(iv) < 1e30 && fabs(iv) > 1e-30 && fabs(m) < 1e30 && fabs(s64) > 1e-30 &&
+                          fabs(s64) < 1e30 && fabs(g) < 1e30;
+        *si = (float)s64;
+        *gln = fits ? (float)(g + (m - e)) : __builtin_nanf("");
+        *glf = fits ? (float)(g + (m + e)) : __builtin_nanf("");
+    };
     float ix = 0.f, iy = 0.f, iz = 0.f, lox = 0.f, loy = 0.f, loz = 0.f, hix = 0.f, hiy = 0.f, hiz = 0.f;
-    if (S32) {
+    if (Q) {
+        axisq(0, r.o.x, inv.x, &ix, &lox, &hix);
+        axisq(1, r.o.y, inv.y, &iy, &loy, &hiy);
+        axisq(2, r.o.z, inv.z, &iz, &loz, &hiz);
+    } else if (S32) {
         axis32(r.o.x, inv.x, &ix, &lox, &hix);
         axis32(r.o.y, inv.y, &iy, &loy, &hiy);
         axis32(r.o.z, inv.z, &iz, &loz, &hiz);
@@ -501,7 +527,31 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // culling stays exact either way.  Small trees keep the test: most of cornell's rays miss its BVH's root
     // (node tests per sample 15.4 -> 20.6 without it).
     int n = any && who >= 0 ? sc.nnodes : (FMA_SLAB && sc.nnodes > 1 ? 1 : 0);
-    while (n < sc.nnodes) {
+    if (Q) {  // the quantized layouts
+        const DNodeQ *qn = (const DNodeQ *)(sc.qnodes + 1) + (size_t)oct * (size_t)sc.nnodes;
+        while (n < sc.nnodes) {
+            const uint4 raw = *(const uint4 *)(qn + n);
+            PT_LP(BVH_NODE);
+            if (STATS) ct->c[C_NODE_SLABS]++;
+            const f2v a = __builtin_elementwise_fma((f2v){(float)(raw.x & 0xffffu), (float)(raw.x >> 16)}, pa_i, pa_m);
+            const f2v b = __builtin_elementwise_fma((f2v){(float)(raw.y & 0xffffu), (float)(raw.y >> 16)}, pb_i, pb_m);
+            const f2v c = __builtin_elementwise_fma((f2v){(float)(raw.z & 0xffffu), (float)(raw.z >> 16)}, pc_i, pc_m);
+            const bool enter = fmaxf(fmaxf(a.x, a.y), fmaxf(b.x, mt32)) <= fminf(fminf(b.y, c.x), fminf(c.y, best32));
+            const uint32_t link = raw.w;
+            if (enter) {
+                PT_LP(BVH_ENTER);
+                if (link >> 31) {  // a leaf
+                    const int first = (int)(link & 0xffffffu), count = (int)(link >> 24 & 0x3fu);
+                    bvh_leaf_test<STATS>(sc, r, axis_ok, first, count, (link >> 30) & 1u, min_t, best, who, ct);
+                    best32 = (float)(best + fabs(best) * 0x1p-20);
+                }
+                n++;
+            } else {
+                n = (link >> 31) ? n + 1 : (int)link;  // a leaf's skip is the next node
+            }
+        }
+    }
+    while (!Q && n < sc.nnodes) {
         const DNodeC nd = nodes[n];
         PT_LP(BVH_NODE);
         if (STATS) ct->c[C_NODE_SLABS]++;

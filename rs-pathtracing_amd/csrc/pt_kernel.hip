@@ -238,6 +238,7 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.shapes = s.shapes;
     d.mats = s.mats;
     d.nodes = s.nodes;
+    d.qnodes = s.qnodes;
     d.leaf = s.leaf;
     d.lin = s.lin;
     d.march = s.march;

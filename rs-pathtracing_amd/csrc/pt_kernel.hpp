@@ -11,6 +11,7 @@ struct DeviceScene {
     DShape *shapes = nullptr;
     DMaterial *mats = nullptr;
     DNodeC *nodes = nullptr;
+    DQGrid *qnodes = nullptr;  // the quantized layouts after their grid (large trees only; else null)
     int32_t *leaf = nullptr, *lin = nullptr, *march = nullptr;
     DBox *boxes = nullptr;
     DTexture *tex = nullptr;  // non-solid textures (null when the scene has none)

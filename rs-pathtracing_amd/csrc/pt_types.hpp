@@ -83,6 +83,24 @@ struct alignas(32) DNodeC {
 };
 static_assert(sizeof(DNodeC) == 32, "DNodeC is half a cache line");
 
+// The large-tree walk's node form (wf_walk, round 5), a quarter cache line: the six planes of a DNodeC as
+// 16-bit steps of a per-axis grid (plane = g0[k] + q * gs[k], gs a power of two covering the root box in 65535
+// steps), lo planes rounded down and hi planes up (the box only grows: the slab test stays conservative), and one
+// link word: an interior node's skip, or a leaf (bit 31; a leaf's skip is always the next node) with bit 30 set
+// for a one-shape leaf whose `first` is the shape id, count in bits 24-29 and first in bits 0-23.
+struct alignas(16) DNodeQ {
+    uint16_t q[6];  // near planes (x, y, z), then far planes, in the octant's order
+    uint32_t link;
+};
+static_assert(sizeof(DNodeQ) == 16, "DNodeQ is a quarter cache line");
+// The quantized nodes' device buffer starts with their grid; the octant layouts follow it.
+struct alignas(64) DQGrid {
+    double g0[3], gs[3];
+    float bound;  // >= |every quantized plane| and >= |g0|
+    float pad[3];
+};
+static_assert(sizeof(DQGrid) == 64, "DQGrid is one cache line");
+
 constexpr int BIG_BVH_NODES = 1 << 15;  // binary nodes from which the bounce runs its large-tree builds (C5)
 
 struct DBox {

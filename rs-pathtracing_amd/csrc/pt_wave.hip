@@ -970,11 +970,14 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // the ray each bounce stored, traced through the uniform list and the BVH
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
+#ifndef PT_WALK_QN
+#define PT_WALK_QN 1  // the walk reads the quantized 16-byte nodes (DNodeQ) when the scene has them (0: DNodeC)
+#endif
 #ifndef PT_WALK_OCT
 #define PT_WALK_OCT 1  // a block's 256 rays regrouped by direction octant before the walk (0: in list order;
                        // 2: by octant and major axis)
 #endif
-template <int WAVES>
+template <int WAVES, bool QN>
 __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__ A, int it) {
     __shared__ uint32_t pos[256];      // the block's list positions, grouped by octant
     constexpr uint32_t NB = PT_WALK_OCT == 2 ? 25u : 9u;  // groups (the last: no ray)
@@ -1030,7 +1033,7 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
-            dev::closest_nomarch<false, false, true>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+            dev::closest_nomarch<false, false, true, QN>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             v.out.t(p) = best;
             uint32_t &w = v.out.who(p);
             w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;
@@ -1743,11 +1746,15 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (split) {  // the new rays' BVH walk, over the live list of it + 1
                     if ((e = timer_begin(ws->timer, cs, K_WALK)) != hipSuccess) return e;
-                    switch (tu.wf_walk) {  // the walk's register budget, waves per SIMD
-                    case 4: wf_walk<4><<<bb, 256, 0, cs>>>(A, it); break;
-                    case 6: wf_walk<6><<<bb, 256, 0, cs>>>(A, it); break;
-                    case 8: wf_walk<8><<<bb, 256, 0, cs>>>(A, it); break;
-                    default: wf_walk<5><<<bb, 256, 0, cs>>>(A, it); break;
+                    if (!(PT_WALK_QN && sc.qnodes)) {  // (a tree without the quantized form)
+                        wf_walk<5, false><<<bb, 256, 0, cs>>>(A, it);
+                    } else {
+                        switch (tu.wf_walk) {  // the walk's register budget, waves per SIMD
+                        case 4: wf_walk<4, true><<<bb, 256, 0, cs>>>(A, it); break;
+                        case 6: wf_walk<6, true><<<bb, 256, 0, cs>>>(A, it); break;
+                        case 8: wf_walk<8, true><<<bb, 256, 0, cs>>>(A, it); break;
+                        default: wf_walk<5, true><<<bb, 256, 0, cs>>>(A, it); break;
+                        }
                     }
                     if ((e = hipGetLastError()) != hipSuccess) return e;
                     if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;

@@ -3,6 +3,7 @@
 // the product's own loader and BVH builder.  Lets the CPU suite compare the
 // GPU algorithm (uniform list + threaded BVH + skipping march + flat sample
 // loop) with the oracle bit for bit.  Never used by the product.
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -15,6 +16,7 @@ using namespace pt;
 struct Bundle {
     Scene sc;
     Accel acc;
+    std::vector<DQGrid> qbuf;  // the quantized layouts after their grid, as the device buffer (DQGrid-aligned)
     std::vector<DShape> shapes;
     std::vector<DMaterial> mats;
     dev::Scene view;
@@ -40,6 +42,16 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.perlin = tex ? b->sc.perlins.data() : nullptr;
         b->view.images = tex ? b->sc.images.data() : nullptr;
         b->view.pixels = tex ? b->sc.pixels.data() : nullptr;
+        if (b->acc.qnodes.empty() && !b->acc.nodes.empty()) build_qnodes(b->acc);  // (small trees too)
+        if (!b->acc.qnodes.empty()) {
+            const size_t nb = b->acc.qnodes.size() * sizeof(DNodeQ);
+            b->qbuf.resize(1 + (nb + sizeof(DQGrid) - 1) / sizeof(DQGrid));
+            DQGrid &g = b->qbuf[0];
+            for (int k = 0; k < 3; k++) g.g0[k] = b->acc.qg0[k], g.gs[k] = b->acc.qgs[k];
+            g.bound = b->acc.qbound;
+            std::memcpy(&b->qbuf[1], b->acc.qnodes.data(), nb);
+            b->view.qnodes = b->qbuf.data();
+        }
         b->view.nnodes = b->acc.nodes_per_octant();
         b->view.bvh_bound = b->acc.bvh_bound;
         b->view.nlin = (int)b->acc.lin.size();
@@ -83,6 +95,40 @@ extern "C" int h_node_check(void *p) {
         ok = ok && count == N[i].count;
         if (fc >> 31) ok = ok && count == 1 && first == b->acc.leaf[N[i].first];
         else ok = ok && first == N[i].first;
+        bad += !ok;
+    }
+    return bad;
+}
+
+// The quantized nodes against the host nodes: every quantized box (g0 + q gs, in f64) must contain the f64 box,
+// an interior node's link must be its skip and a leaf's must decode to its shapes.  Returns the failures (0
+// expected), or -1 without quantized nodes.
+extern "C" int h_qnode_check(void *p) {
+    Bundle *b = (Bundle *)p;
+    const auto &N = b->acc.nodes;
+    const auto &Q = b->acc.qnodes;
+    const auto &Cn = b->acc.cnodes;
+    if (Q.size() != N.size() || N.empty()) return -1;
+    const size_t per = N.size() / BVH_OCTANTS;
+    int bad = 0;
+    for (size_t i = 0; i < N.size(); i++) {
+        const int oct = (int)(i / per);
+        bool ok = true;
+        for (int k = 0; k < 3; k++) {
+            const bool neg = (oct >> k) & 1;
+            const double ql = neg ? Q[i].q[3 + k] : Q[i].q[k], qh = neg ? Q[i].q[k] : Q[i].q[3 + k];
+            const double lo = b->acc.qg0[k] + ql * b->acc.qgs[k], hi = b->acc.qg0[k] + qh * b->acc.qgs[k];
+            ok = ok && lo <= N[i].lo[k] && hi >= N[i].hi[k] && std::fabs(lo) <= b->acc.qbound &&
+                 std::fabs(hi) <= b->acc.qbound;
+        }
+        const uint32_t l = Q[i].link;
+        if (N[i].count == 0) {
+            ok = ok && !(l >> 31) && (int32_t)l == N[i].skip;
+        } else {
+            const uint32_t fc = Cn[i].first_count;
+            ok = ok && (l >> 31) && (int)(l >> 24 & 0x3fu) == N[i].count && (l & 0xffffffu) == (fc & 0xffffffu) &&
+                 ((l >> 30) & 1u) == (fc >> 31) && (size_t)N[i].skip == i % per + 1;
+        }
         bad += !ok;
     }
     return bad;
@@ -178,7 +224,10 @@ extern "C" int h_closest_nomarch(void *p, const double *ray, int fma, double *t)
     const dev::V3 inv = dev::v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
     double best = __builtin_inf();
     int who = -1;
-    if (fma) {
+    if (fma == 2) {  // the quantized nodes (wf_walk's build)
+        if (!b->view.qnodes) return -2;
+        dev::closest_nomarch<false, false, true, true>(b->view, r, inv, T_MIN, &best, &who);
+    } else if (fma) {
         dev::closest_nomarch<false, false, true>(b->view, r, inv, T_MIN, &best, &who);
     } else {
         dev::closest_nomarch<false, false, false>(b->view, r, inv, T_MIN, &best, &who);

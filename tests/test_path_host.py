@@ -251,12 +251,24 @@ def test_bvh_fma_slab_build_same_hits(H):
             d = np.where(d == 0, rng.choice([0.0, -0.0, 1e-300, rng.normal() * 0.3], size=3), d)
         d /= np.linalg.norm(d)
         ray = (C.c_double * 6)(*np.concatenate([o, d]))
-        t0, t1 = C.c_double(), C.c_double()
+        t0, t1, t2 = C.c_double(), C.c_double(), C.c_double()
         w0 = H.h_closest_nomarch(pr.h, ray, 0, C.byref(t0))
         w1 = H.h_closest_nomarch(pr.h, ray, 1, C.byref(t1))
-        assert (w0, t0.value) == (w1, t1.value), (o, d)
+        w2 = H.h_closest_nomarch(pr.h, ray, 2, C.byref(t2))  # the quantized nodes (wf_walk)
+        assert (w0, t0.value) == (w1, t1.value) == (w2, t2.value), (o, d)
         hits += w0 >= 0
     assert hits > 1000
+
+
+def test_quantized_nodes_contain_the_boxes(H):
+    """The 16-byte nodes of the large-tree walk (DNodeQ): every box on the per-axis grid contains the node's f64
+    box (lo rounded down, hi up), interior links are the skips and leaf links decode to the leaf's shapes."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    H.h_qnode_check.argtypes = [C.c_void_p]
+    pr = Pair(H, json.dumps(make_scenes.synthetic(3000)), seed=1)
+    assert H.h_qnode_check(pr.h) == 0
 
 
 def test_bvh_fma_slab_tiny_direction_component(H):
@@ -289,7 +301,7 @@ def test_bvh_fma_slab_tiny_direction_component(H):
         ray6 = np.concatenate([o, d])
         ray = (C.c_double * 6)(*ray6)
         ref = pr.o.closest_hit(o, d)
-        for fma in (0, 1):
+        for fma in (0, 1, 2):
             t = C.c_double()
             w = H.h_closest_nomarch(pr.h, ray, fma, C.byref(t))
             if ref is None:
@@ -301,7 +313,8 @@ def test_bvh_fma_slab_tiny_direction_component(H):
 
 
 def test_large_tree_walk_far_origins_and_grazing_rays(H):
-    """The large-tree walk (fma = 1: FMA_SLAB, with PT_SLAB32 its f32 slab widened by the error bound) keeps
+    """The large-tree walk (fma = 1: FMA_SLAB, with PT_SLAB32 its f32 slab widened by the error bound; fma = 2:
+    the quantized nodes, their grid folded into the widened offsets) keeps
     every node that holds the closest hit: rays from origins up to 1e5 away, aimed to graze spheres' silhouettes
     (|t| large, planes far from the origin), and rays leaving from sphere surfaces at shallow angles."""
     import sys
@@ -330,9 +343,10 @@ def test_large_tree_walk_far_origins_and_grazing_rays(H):
             d = np.cross(n, rng.normal(size=3)) + n * rng.uniform(1e-9, 1e-3)  # nearly tangent
         d /= np.linalg.norm(d)
         ray = (C.c_double * 6)(*np.concatenate([o, d]))
-        t0, t1 = C.c_double(), C.c_double()
+        t0, t1, t2 = C.c_double(), C.c_double(), C.c_double()
         w0 = H.h_closest_nomarch(pr.h, ray, 0, C.byref(t0))
         w1 = H.h_closest_nomarch(pr.h, ray, 1, C.byref(t1))
-        assert (w0, t0.value) == (w1, t1.value), (o, d)
+        w2 = H.h_closest_nomarch(pr.h, ray, 2, C.byref(t2))  # the quantized nodes (wf_walk)
+        assert (w0, t0.value) == (w1, t1.value) == (w2, t2.value), (o, d)
         hits += w0 >= 0
     assert hits > 500

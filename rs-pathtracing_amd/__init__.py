@@ -539,7 +539,7 @@ def option_names() -> list:
 
 
 # the defaults (pt_kernel.hpp Tuning): bench.py reports knobs that differ
-OPTION_DEFAULTS = {"engine": 0, "mega_waves": 4, "diag": 0, "wf_slots": 2, "wf_paths": 3 << 24, "wf_min_chunks": 1,
+OPTION_DEFAULTS = {"engine": 0, "mega_waves": 4, "diag": 0, "wf_slots": 2, "wf_paths": 0, "wf_min_chunks": 1,
                    "wf_bounce_waves": 3, "wf_march_slice": 256,
                    "wf_march_blocks_per_cu": 0, "wf_side_priority": 0,
                    "wf_pingpong": 0, "wf_stagger": 0, "wf_tail_paths": 0, "wf_walk": 5, "bvh_leaf": 1}

@@ -355,7 +355,9 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out, int *fault = nul
         g.bound = acc.qbound;
         const size_t nb = acc.qnodes.size() * sizeof(DNodeQ);
         if (fault && *fault > 0 && (*fault)-- == 1) err = hipErrorOutOfMemory;
-        if (err == hipSuccess) err = hipMalloc((void **)&a.qnodes, sizeof(DQGrid) + nb);
+        // (one node of padding past the last layout: the walk may load node n + 1 ahead, PT_WALK_PREFETCH)
+        if (err == hipSuccess) err = hipMalloc((void **)&a.qnodes, sizeof(DQGrid) + nb + sizeof(DNodeQ));
+        if (err == hipSuccess) err = hipMemset((char *)(a.qnodes + 1) + nb, 0, sizeof(DNodeQ));
         if (err == hipSuccess) err = hipMemcpy(a.qnodes, &g, sizeof g, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(a.qnodes + 1, acc.qnodes.data(), nb, hipMemcpyHostToDevice);
     }

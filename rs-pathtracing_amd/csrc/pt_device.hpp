@@ -98,6 +98,9 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 #ifndef PT_RECT_SIGN
 #define PT_RECT_SIGN 0  // rectangles: rays moving away from the plane rejected before the division (round 5 A/B: C2 2061 -> 2034, off)
 #endif
+#ifndef PT_WALK_PREFETCH
+#define PT_WALK_PREFETCH 0  // the quantized walk loads node n + 1 with node n
+#endif
 #ifndef PT_AXIS_LEAF
 #define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,
                         // 2 in the large-tree (FMA_SLAB) builds only (C5 +3.2 %; in the C2 bounce the extra path
@@ -529,8 +532,12 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     int n = any && who >= 0 ? sc.nnodes : (FMA_SLAB && sc.nnodes > 1 ? 1 : 0);
     if (Q) {  // the quantized layouts
         const DNodeQ *qn = (const DNodeQ *)(sc.qnodes + 1) + (size_t)oct * (size_t)sc.nnodes;
+        // PT_WALK_PREFETCH: node n + 1 (where an entered node leads) is loaded with node n, so a descent's next
+        // node is in flight while this one is tested (the buffer holds one node of padding past the layouts)
+        uint4 raw_next = PT_WALK_PREFETCH && n < sc.nnodes ? *(const uint4 *)(qn + n) : make_uint4(0, 0, 0, 0);
         while (n < sc.nnodes) {
-            const uint4 raw = *(const uint4 *)(qn + n);
+            const uint4 raw = PT_WALK_PREFETCH ? raw_next : *(const uint4 *)(qn + n);
+            if (PT_WALK_PREFETCH) raw_next = *(const uint4 *)(qn + n + 1);
             PT_LP(BVH_NODE);
             if (STATS) ct->c[C_NODE_SLABS]++;
             const f2v a = __builtin_elementwise_fma((f2v){(float)(raw.x & 0xffffu), (float)(raw.x >> 16)}, pa_i, pa_m);
@@ -548,6 +555,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
                 n++;
             } else {
                 n = (link >> 31) ? n + 1 : (int)link;  // a leaf's skip is the next node
+                if (PT_WALK_PREFETCH && !(link >> 31) && n < sc.nnodes) raw_next = *(const uint4 *)(qn + n);
             }
         }
     }

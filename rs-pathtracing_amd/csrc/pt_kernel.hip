@@ -304,8 +304,8 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
     };
     *iv = nullptr;
     if (!name) return nullptr;
-    if (!strcmp(name, "wf_paths")) {
-        *lo = 256;
+    if (!strcmp(name, "wf_paths")) {  // (0 = by depth; 1..255 refused in tuning_set)
+        *lo = 0;
         *hi = (int64_t)1 << 28;
         return &t->wf_paths;
     }
@@ -333,6 +333,7 @@ int tuning_set(Tuning *t, const char *name, int64_t v) {
     if (!strcmp(name, "wf_bounce_waves") && !(v == 2 || v == 3 || v == 4 || v == 5 || v == 6 || v == 8))
         return PT_ERR_INVALID;
     if (!strcmp(name, "wf_walk") && !(v == 0 || v == 4 || v == 5 || v == 6 || v == 8)) return PT_ERR_INVALID;
+    if (!strcmp(name, "wf_paths") && v > 0 && v < 256) return PT_ERR_INVALID;
     if (lv) *lv = v;
     else *iv = (int)v;
     return PT_OK;

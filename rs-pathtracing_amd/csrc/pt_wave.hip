@@ -1489,7 +1489,8 @@ template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws, int fkind) {
     const Tuning &tu = ws->tune;
-    const uint32_t cap_want = (uint32_t)tu.wf_paths;
+    // path slots per chunk: Tuning::wf_paths, or by depth (deep frames: bigger chunks, fewer tails)
+    const uint32_t cap_want = tu.wf_paths ? (uint32_t)tu.wf_paths : (P0.depth > 16 ? 1u << 27 : 3u << 24);
     // the launch's samples: the frame's, or a resumable frame's window [s_begin, s_end) of them
     const uint32_t s_begin = P0.s_begin, s_end = P0.s_end ? P0.s_end : P0.spp, nsw = s_end - s_begin;
     // tile groups (only for frames beyond cap_want pixels), then sample chunks
@@ -1505,8 +1506,10 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         // least wf_min_chunks sample chunks, so the pipelined slots overlap one
         // chunk's short tail iterations with the next chunk's work; chunks
         // keep at least MIN_CHUNK_PATHS paths to fill the device.
-        // (a progressive frame's band, P0.stop set, gets at least two: one per chunk stream)
-        const uint32_t mc = P0.stop && tu.wf_min_chunks < 2 ? 2u : (uint32_t)tu.wf_min_chunks;
+        // (a progressive frame's band, P0.stop set, gets at least two: one per chunk stream; and any frame at
+        // least one per chunk stream while its chunks keep MIN_CHUNK_PATHS paths, whatever wf_paths allows)
+        uint32_t mc = P0.stop && tu.wf_min_chunks < 2 ? 2u : (uint32_t)tu.wf_min_chunks;
+        if (mc < (uint32_t)tu.wf_slots) mc = (uint32_t)tu.wf_slots;
         if (mc > 1 && ntiles <= group_tiles) {
             uint32_t want = (nsw + mc - 1) / mc;
             const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;

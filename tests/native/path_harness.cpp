@@ -45,7 +45,7 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         if (b->acc.qnodes.empty() && !b->acc.nodes.empty()) build_qnodes(b->acc);  // (small trees too)
         if (!b->acc.qnodes.empty()) {
             const size_t nb = b->acc.qnodes.size() * sizeof(DNodeQ);
-            b->qbuf.resize(1 + (nb + sizeof(DQGrid) - 1) / sizeof(DQGrid));
+            b->qbuf.resize(2 + (nb + sizeof(DQGrid) - 1) / sizeof(DQGrid));  // (+ padding past the layouts)
             DQGrid &g = b->qbuf[0];
             for (int k = 0; k < 3; k++) g.g0[k] = b->acc.qg0[k], g.gs[k] = b->acc.qgs[k];
             g.bound = b->acc.qbound;

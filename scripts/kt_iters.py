@@ -11,7 +11,10 @@ count_work probe are counted.
 """
 import collections
 import csv
+import re
 import sys
+
+FIRST = re.compile(r"wf_bounce<\d+, true")  # a chunk's first-iteration bounce (the FIRST template argument)
 
 
 def main():
@@ -26,7 +29,7 @@ def main():
         name = r["Kernel_Name"]
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         if "wf_bounce" in name:
-            if ", true," in name:
+            if FIRST.search(name):
                 it = 0
                 chunks += 1
             else:

@@ -10,18 +10,22 @@ start with one first-iteration bounce launch (wf_bounce<.., true, ..>).
 """
 import collections
 import csv
+import re
 import sys
+
+FIRST = re.compile(r"wf_bounce<\d+, true")  # a chunk's first-iteration bounce (the FIRST template argument)
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 total_frames = int(sys.argv[2])
 end = max(i for i, r in enumerate(rows) if "count_work" in r["Kernel_Name"])
-firsts = [i for i in range(end) if "wf_bounce" in rows[i]["Kernel_Name"] and ", true," in rows[i]["Kernel_Name"]]
+firsts = [i for i in range(end) if FIRST.search(rows[i]["Kernel_Name"])]
 chunks = len(firsts) // total_frames
 start = firsts[-chunks]
 agg = collections.defaultdict(lambda: [0, 0.0])
 for r in rows[start:end]:
     name = r["Kernel_Name"]
     key = ("wf_bounce" if "wf_bounce" in name else "wf_march" if "wf_march" in name else
+           "wf_walk" if "wf_walk" in name else "wf_tail" if "wf_tail" in name else
            "compaction" if "cp_" in name else "wf_reduce" if "wf_reduce" in name else name[:40])
     agg[key][0] += 1
     agg[key][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6

@@ -306,10 +306,6 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
         }
         rest.swap(keep);
     }
-    // the uniform list's rectangles first (the acceptance rule makes the visiting order free): the walk tests
-    // them two at a time (dev::closest_nomarch)
-    std::stable_partition(a.lin.begin(), a.lin.end(), [&](int32_t i) { return sc.shapes[i].type == RECTANGLE; });
-    a.lin_rects = (int)std::count_if(a.lin.begin(), a.lin.end(), [&](int32_t i) { return sc.shapes[i].type == RECTANGLE; });
     if (!rest.empty()) {
         Builder b{a.boxes, a};
         b.leaf_max = std::max(1, std::min(16, leaf_max));

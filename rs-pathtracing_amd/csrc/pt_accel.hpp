@@ -34,8 +34,7 @@ struct Accel {
     std::vector<DNodeC> cnodes;  // the same nodes in the device form (f32 boxes rounded outward)
     int nodes_per_octant() const { return (int)(nodes.size() / BVH_OCTANTS); }
     std::vector<int32_t> leaf;   // shape ids referenced by leaf nodes
-    std::vector<int32_t> lin;    // wave-uniform list (its rectangles first: lin_rects of them)
-    int lin_rects = 0;
+    std::vector<int32_t> lin;    // wave-uniform list
     std::vector<int32_t> march;  // ray-marched shapes
     std::vector<DBox> boxes;     // padded world AABB per shape
     float bvh_bound = 0.f;  // >= |every plane of cnodes| (dev::Scene::bvh_bound)

@@ -318,7 +318,6 @@ struct StagedAccel {
     DBox *boxes = nullptr;
     int nnodes = 0, nlin = 0, nmarch = 0;
     float bvh_bound = 0.f;
-    int nlin_rect = 0;
 };
 
 // Test hook (renderer option "fault_accel_alloc" = n, kept per renderer): the
@@ -368,7 +367,6 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out, int *fault = nul
     }
     a.nnodes = acc.nodes_per_octant();  // nodes per octant layout
     a.nlin = (int)acc.lin.size();
-    a.nlin_rect = acc.lin_rects;
     a.nmarch = (int)acc.march.size();
     a.bvh_bound = acc.bvh_bound;
     *out = a;
@@ -381,8 +379,7 @@ int commit_accel(GpuShare &g, StagedAccel &a) {
     HIP_TRY(hipSetDevice(g.device));
     HIP_TRY(hipDeviceSynchronize());
     DeviceScene &d = g.ds;
-    StagedAccel old{d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.bvh_bound,
-                    d.nlin_rect};
+    StagedAccel old{d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.nnodes, d.nlin, d.nmarch, d.bvh_bound};
     d.nodes = a.nodes;
     d.qnodes = a.qnodes;
     d.leaf = a.leaf;
@@ -391,7 +388,6 @@ int commit_accel(GpuShare &g, StagedAccel &a) {
     d.boxes = a.boxes;
     d.nnodes = a.nnodes;
     d.nlin = a.nlin;
-    d.nlin_rect = a.nlin_rect;
     d.nmarch = a.nmarch;
     d.bvh_bound = a.bvh_bound;
     a = StagedAccel{};

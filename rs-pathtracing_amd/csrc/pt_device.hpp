@@ -101,9 +101,6 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
 #ifndef PT_WALK_PREFETCH
 #define PT_WALK_PREFETCH 0  // the quantized walk loads node n + 1 with node n
 #endif
-#ifndef PT_RECT_PAIRS
-#define PT_RECT_PAIRS 1  // the uniform list's rectangles tested two at a time (closest_nomarch)
-#endif
 #ifndef PT_AXIS_LEAF
 #define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,
                         // 2 in the large-tree (FMA_SLAB) builds only (C5 +3.2 %; in the C2 bounce the extra path
@@ -220,29 +217,6 @@ PT_HD void note_stop(unsigned long long *counters, bool worked) {
 #endif
 }
 
-// Rectangle: t needs only the object-space z row (rect_t), x and y are transformed only for a t in range.  Each
-// component is the same expression as in xf_point / xf_vector, so every value is unchanged.  rect_rest: the range
-// test of tt = -oz / dz and the in-rectangle test.
-PT_HD double rect_t(const DShape &s, const Ray &r) {
-    const double *m = s.inv;
-    const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
-    const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
-    return -oz / dz;
-}
-PT_HD bool rect_rest(const DShape &s, const Ray &r, double tt, double min_t, double max_t, double *t) {
-    if (tt < min_t || tt > max_t) return false;
-    PT_LP(RECT_ROWS);
-    const double *m = s.inv;
-    const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
-    const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
-    const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
-    const double dy = r.d.x * m[4] + r.d.y * m[5] + r.d.z * m[6];
-    const double px = ox + dx * tt, py = oy + dy * tt;
-    if (px < s.p[0] || px > s.p[2] || py < s.p[1] || py > s.p[3]) return false;
-    *t = tt;
-    return true;
-}
-
 // MARCHED=false: the caller's lists hold no ray-marched shape (build_accel puts
 // every one on the march list), so the march branch is not compiled in.
 // EXT: the extended build (scenes with a Torus or non-solid textures) that
@@ -252,6 +226,9 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
                       unsigned long long *guard = nullptr) {
     if (STATS) ct->c[s.type == TORUS ? C_TEST_TORUS : C_TEST_SPHERE + s.type]++;
     if (s.type == RECTANGLE) {
+        // Rectangle: t needs only the object-space z row; x and y are
+        // transformed only for a t in range.  Each component is the same
+        // expression as in xf_point / xf_vector, so every value is unchanged.
         const double *m = s.inv;
         const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
@@ -259,7 +236,17 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         // positive min_t: rejected without the division (NaN and dz = 0, the range test's quirk, go on)
         if (PT_RECT_SIGN && min_t > 0.0 && dz != 0.0 && dz == dz && oz == oz && (oz == 0.0 || (oz < 0.0) == (dz < 0.0)))
             return false;
-        return rect_rest(s, r, -oz / dz, min_t, max_t, t);
+        const double tt = -oz / dz;
+        if (tt < min_t || tt > max_t) return false;
+        PT_LP(RECT_ROWS);
+        const double ox = r.o.x * m[0] + r.o.y * m[1] + r.o.z * m[2] + m[3];
+        const double oy = r.o.x * m[4] + r.o.y * m[5] + r.o.z * m[6] + m[7];
+        const double dx = r.d.x * m[0] + r.d.y * m[1] + r.d.z * m[2];
+        const double dy = r.d.x * m[4] + r.d.y * m[5] + r.d.z * m[6];
+        const double px = ox + dx * tt, py = oy + dy * tt;
+        if (px < s.p[0] || px > s.p[2] || py < s.p[1] || py > s.p[3]) return false;
+        *t = tt;
+        return true;
     }
     V3 o = xf_point(s.inv, r.o);  // inverse_transform_ray (transform.rs:32-37), no renormalisation
     V3 d = xf_vector(s.inv, r.d);
@@ -369,7 +356,6 @@ struct Scene {
     const DImage *__restrict__ images;
     const uint8_t *__restrict__ pixels;
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
-    int nlin_rect;                   // lin's leading rectangles (pt_accel.cpp puts them first)
     int nmats;
     int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
     float bvh_bound;  // >= |every BVH node plane| (the f32 slab's error bound, PT_SLAB32)
@@ -437,28 +423,8 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
                            Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
     int who = *who_out;
-    // wave-uniform list (few JSON shapes): scalar loads of each shape.  PT_RECT_PAIRS: its leading rectangles two
-    // at a time, both divisions before either range test (two independent chains in flight), the second tested
-    // against the best hit the first may have set
-    int k0 = 0;
-    if (PT_RECT_PAIRS && !STATS) {
-        for (; k0 + 1 < sc.nlin_rect; k0 += 2) {
-            if (any && wave_all(who >= 0)) break;
-            const int i0 = uniform_index(uniform_load(&sc.lin[k0])), i1 = uniform_index(uniform_load(&sc.lin[k0 + 1]));
-            const DShape s0 = uniform_shape(&sc.shapes[i0]), s1 = uniform_shape(&sc.shapes[i1]);
-            const double t0 = rect_t(s0, r), t1 = rect_t(s1, r);
-            double t;
-            if (rect_rest(s0, r, t0, min_t, best, &t) && (t < best || i0 > who)) {
-                best = t;
-                who = i0;
-            }
-            if (rect_rest(s1, r, t1, min_t, best, &t) && (t < best || i1 > who)) {
-                best = t;
-                who = i1;
-            }
-        }
-    }
-    for (int k = k0; k < sc.nlin; k++) {
+    // wave-uniform list (few JSON shapes): scalar loads of each shape
+    for (int k = 0; k < sc.nlin; k++) {
         if (any && wave_all(who >= 0)) break;
         const int i = uniform_index(uniform_load(&sc.lin[k]));
         const DShape s = uniform_shape(&sc.shapes[i]);

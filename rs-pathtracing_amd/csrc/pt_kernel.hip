@@ -251,7 +251,6 @@ static dev::Scene dscene(const DeviceScene &s) {
     d.nnodes = s.nnodes;
     d.bvh_bound = s.bvh_bound;
     d.nlin = s.nlin;
-    d.nlin_rect = s.nlin_rect;
     d.nmarch = s.nmarch;
     d.nmats = s.nmats;
     d.diag = s.diag;

@@ -19,7 +19,6 @@ struct DeviceScene {
     DImage *images = nullptr;
     uint8_t *pixels = nullptr;
     int nshapes = 0, nmats = 0, nnodes = 0, nlin = 0, nmarch = 0;
-    int nlin_rect = 0;  // the uniform list's leading rectangles
     float bvh_bound = 0.f;  // Accel::bvh_bound
     int ext = 0;    // non-solid textures or a Torus: the extended (EXT) kernel builds
     int fkind = 0;  // 0: every marched shape is a Heart (or none) -> Heart-only kernel builds; -1: any

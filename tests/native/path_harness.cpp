@@ -55,7 +55,6 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.nnodes = b->acc.nodes_per_octant();
         b->view.bvh_bound = b->acc.bvh_bound;
         b->view.nlin = (int)b->acc.lin.size();
-        b->view.nlin_rect = b->acc.lin_rects;
         b->view.nmarch = (int)b->acc.march.size();
         b->view.diag = 0;
         b->s11 = uniform_incl_scale(-1.0, 1.0);

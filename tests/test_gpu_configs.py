@@ -113,6 +113,9 @@ def test_c5_synthetic_100k_spheres(pt, c5):
     for walk in (0, 4, 5, 6, 8):
         r.set_option("wf_walk", walk)
         assert np.array_equal(r.render(cam, pt.ImageParams(160, 90), 2, seed=2), ref), walk
+    r.set_option("wf_walk", 5)
+    r.set_option("bvh_leaf", 3)  # multi-shape leaves in the quantized nodes' links
+    assert np.array_equal(r.render(cam, pt.ImageParams(160, 90), 2, seed=2), ref)
 
 
 def test_shard_pixels_matches_device_deal(pt, cornell):

@@ -418,13 +418,15 @@ PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first,
 // QN (with FMA_SLAB and PT_SLAB32; sc.qnodes set): the BVH walk reads the quantized nodes (DNodeQ), 16 bytes
 // instead of 32: t = fma(q, gs / d, (g0 - o) / d -/+ e') per plane, the same culling with the grid folded into
 // the per-ray offsets and a wider margin (below).
-template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false, bool QN = false>
+// PART: bit 0 the uniform list, bit 1 the BVH (PT_WALK_ULIST_IN_BOUNCE: the split bounce traces the uniform list,
+// wf_walk the BVH).
+template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false, bool QN = false, int PART = 3>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
                            Ctr *ct = nullptr, bool any = false) {
     double best = *best_t;
     int who = *who_out;
     // wave-uniform list (few JSON shapes): scalar loads of each shape
-    for (int k = 0; k < sc.nlin; k++) {
+    for (int k = 0; k < ((PART & 1) ? sc.nlin : 0); k++) {
         if (any && wave_all(who >= 0)) break;
         const int i = uniform_index(uniform_load(&sc.lin[k]));
         const DShape s = uniform_shape(&sc.shapes[i]);
@@ -530,6 +532,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // culling stays exact either way.  Small trees keep the test: most of cornell's rays miss its BVH's root
     // (node tests per sample 15.4 -> 20.6 without it).
     int n = any && who >= 0 ? sc.nnodes : (FMA_SLAB && sc.nnodes > 1 ? 1 : 0);
+    if (!(PART & 2)) n = sc.nnodes;
     if (Q) {  // the quantized layouts
         const DNodeQ *qn = (const DNodeQ *)(sc.qnodes + 1) + (size_t)oct * (size_t)sc.nnodes;
         // PT_WALK_PREFETCH: node n + 1 (where an entered node leads) is loaded with node n, so a descent's next

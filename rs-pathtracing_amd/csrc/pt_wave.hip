@@ -411,9 +411,14 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
                 }
             }
         }
-        if (live && SPLIT) {  // the ray is traced by wf_walk (pending hit: none yet)
+        if (live && SPLIT) {  // the ray is traced by wf_walk (PT_WALK_ULIST_IN_BOUNCE: the uniform list here)
             best = __builtin_inf();
             who = -1;
+            if (PT_WALK_ULIST_IN_BOUNCE) {
+                const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
+                dev::closest_nomarch<false, false, true, false, 1>(kargs(A).sc, ray, inv, T_MIN, &best, &who, nullptr,
+                                                                   depth == 0);
+            }
         } else if (live) {
             PT_LP(TRACE);
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
@@ -970,6 +975,9 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // the ray each bounce stored, traced through the uniform list and the BVH
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
+#ifndef PT_WALK_ULIST_IN_BOUNCE
+#define PT_WALK_ULIST_IN_BOUNCE 0  // the split bounce traces the uniform list, wf_walk only the BVH
+#endif
 #ifndef PT_WALK_QN
 #define PT_WALK_QN 1  // the walk reads the quantized 16-byte nodes (DNodeQ) when the scene has them (0: DNodeC)
 #endif
@@ -1033,7 +1041,12 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
-            dev::closest_nomarch<false, false, true, QN>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
+            if (PT_WALK_ULIST_IN_BOUNCE) {  // the bounce's uniform-list hit
+                best = d[PathSoA::T * B];
+                who = unpack_who(v.out.who(p));
+            }
+            dev::closest_nomarch<false, false, true, QN, PT_WALK_ULIST_IN_BOUNCE ? 2 : 3>(a.sc, ray, inv, T_MIN, &best,
+                                                                                          &who, nullptr, any);
             v.out.t(p) = best;
             uint32_t &w = v.out.who(p);
             w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;

@@ -152,3 +152,9 @@ def test_plain_c_caller_checkpoint(tmp_path):
     out = subprocess.run([abi_check_bin(), "checkpoint", str(tmp_path / "f.ckpt")], capture_output=True, text=True)
     assert out.returncode == 0, (out.returncode, out.stderr)
     assert "checkpoint round trip" in out.stdout and "corrupt file refused" in out.stdout
+
+
+def test_option_names_match_the_python_defaults(pt):
+    """Every tuning knob the library names (pt_option_name) has a default in the Python mirror and vice versa
+    (no GPU needed)."""
+    assert set(pt.option_names()) == set(pt.OPTION_DEFAULTS)

@@ -300,6 +300,12 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 #endif
 constexpr int WF_PREDICT = PT_WF_PREDICT;
 
+#ifndef PT_WALK_ULIST_IN_BOUNCE
+#define PT_WALK_ULIST_IN_BOUNCE 0  // the split bounce traces the uniform list, wf_walk only the BVH
+#endif
+#ifndef PT_WALK_XCD
+#define PT_WALK_XCD 0  // XCD-aware block order in the walk kernel
+#endif
 #ifndef PT_MARCH_SPREAD
 #define PT_MARCH_SPREAD 1  // a short march queue dealt in runs of count / blocks (1), or always in slice runs (0)
 #endif
@@ -975,9 +981,6 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // the ray each bounce stored, traced through the uniform list and the BVH
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
-#ifndef PT_WALK_ULIST_IN_BOUNCE
-#define PT_WALK_ULIST_IN_BOUNCE 0  // the split bounce traces the uniform list, wf_walk only the BVH
-#endif
 #ifndef PT_WALK_QN
 #define PT_WALK_QN 1  // the walk reads the quantized 16-byte nodes (DNodeQ) when the scene has them (0: DNodeC)
 #endif
@@ -994,7 +997,12 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
     const uint32_t stride = gridDim.x * blockDim.x;
     // the trace after bounce it is shaded at depth P.depth - it: at 0 only hit or miss matters
     const bool any = kargs(A).P.depth == (uint32_t)it;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {  // (block-uniform)
+    // PT_WALK_XCD: the workgroups are dealt to the 8 XCDs round-robin by id, so block b takes the rays of logical
+    // block (b mod 8) * (blocks / 8) + b / 8: each XCD walks a contiguous (pixel-coherent) eighth of every
+    // grid-wide round, and its own L2 holds that region's nodes
+    const uint32_t lb = PT_WALK_XCD && gridDim.x % 8u == 0 ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u
+                                                          : blockIdx.x;
+    for (uint32_t base = lb * blockDim.x; base < count; base += stride) {  // (block-uniform)
         const WfArgs &a = kargs(A);
         const WfView &v = a.v;
         const uint32_t i = base + threadIdx.x;

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE", help="renderer option (A/B)")
     a = ap.parse_args()
 
     import __graft_entry__ as ge
@@ -60,6 +61,9 @@ def main():
     text = (ROOT / "scenes" / a.scene).read_text()
     scene = pt.Scene.from_json(text, seed=1)
     r = pt.HipRenderer(scene, depth=DEPTH)
+    for o in a.option:
+        k, v = o.split("=")
+        r.set_option(k, int(v))
     cam = scene.camera()
     buf = np.zeros((W * H, 3))
     rgba = np.zeros((W * H, 4), dtype=np.uint8)

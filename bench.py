@@ -159,6 +159,35 @@ def launch_plan(args, env):
     return "one"
 
 
+def device_topology(infos, backend, comm_size):
+    """What the ranks of a multi-rank bench ran on: each rank's LOCAL_RANK, device ordinal, PCI address and UUID
+    (gathered to every rank), the backend and the communicator size, and the groups of ranks that shared one
+    physical device (by UUID, else PCI address)."""
+    by_dev = {}
+    for i in infos:
+        by_dev.setdefault(i.get("uuid") or i.get("pci"), []).append(i["rank"])
+    shared = sorted(sorted(v) for v in by_dev.values() if len(v) > 1)
+    return {"backend": backend, "comm_size": comm_size, "ranks": sorted(infos, key=lambda i: i["rank"]),
+            "distinct_devices": len(by_dev), "shared_devices": shared}
+
+
+def topology_refusal(topo):
+    """Under nccl (RCCL) every rank must own its GPU: a bench line whose ranks shared one would not measure N
+    GPUs.  None when the topology is acceptable; gloo rehearsals may share the box's GPU."""
+    if topo["backend"] == "nccl" and topo["shared_devices"]:
+        return ("bench.py: %d ranks over nccl (RCCL) but only %d distinct GPUs: ranks %s share a device"
+                % (topo["comm_size"], topo["distinct_devices"], topo["shared_devices"]))
+    if topo["comm_size"] != len(topo["ranks"]):
+        return "bench.py: communicator size %d but %d ranks reported" % (topo["comm_size"], len(topo["ranks"]))
+    return None
+
+
+def device_identity(torch, ordinal):
+    p = torch.cuda.get_device_properties(ordinal)
+    return {"device": ordinal, "name": p.name,
+            "pci": "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id), "uuid": str(p.uuid)}
+
+
 def device_shortfall(world, backend, ndev):
     """The error for `world` ranks on `ndev` visible devices, or None: RCCL needs one GPU per rank; gloo ranks may
     share one (a rehearsal of the rank path)."""
@@ -367,6 +396,17 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    topo = None
+    if world > 1:  # which physical GPU each rank renders on, as every rank sees it
+        mine = dict(device_identity(torch, local), rank=rank, local_rank=int(os.environ.get("LOCAL_RANK", "0")))
+        infos = [None] * world
+        dist.all_gather_object(infos, mine)
+        topo = device_topology(infos, "gloo" if gloo else "nccl", dist.get_world_size())
+        why = topology_refusal(topo)
+        if why:
+            if rank == 0:
+                print(why, file=sys.stderr, flush=True)
+            sys.exit(3)
 
     import __graft_entry__ as ge
     pt = ge.load_package()
@@ -569,9 +609,14 @@ def main():
                          "events_per_sample": {k: round(v / max(1, counts["samples"]), 3)
                                                for k, v in counts.items() if k != "samples"},
                          # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
-                         # launches overlap the other kind's; the whole path's rate is the frame's FLOPs over
-                         # the frame time
-                         "timed_kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in kt.items()},
+                         # launches overlap the other stream's; these sums of launch durations can exceed the
+                         # step time, and the whole path's rate is the frame's FLOPs over the frame time
+                         "timed_kernel_ms_per_step_summed_over_streams": {k: round(v[0] / args.steps, 3)
+                                                                          for k, v in kt.items()},
+                         "timed_kernel_ms_note": ("launch durations summed per kernel kind over %d concurrent "
+                                                  "chunk streams: they overlap, so a sum may exceed ms_per_step; "
+                                                  "per-kernel times of launches that run alone are in `kernels`"
+                                                  % slots),
                          "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3),
                          "path_achieved": round(F * value * 1e6 / 1e12, 4),
                          "path_frac": round(F * value * 1e6 / 1e12 / FP64_PEAK_TFLOPS, 5)},
@@ -593,7 +638,11 @@ def main():
                              "what": ("dist.gather of the compact f64 shards to rank 0 (%s) + pt_unshard_device, "
                                       "HIP events on rank 0's stream" % ("gloo, through host memory" if gloo
                                                                          else "RCCL"))}
+        if topo is not None:
+            rec["topology"] = topo
         if multi:
+            rec["topology"] = {"backend": "one process, peer copies", "devices": [
+                device_identity(torch, d) for d in range(args.gpus)]}
             pairs, enabled = r.peer_access()
             rec["gather"] = {"bytes_total": args.gpus * pt.shard_tiles(W, H, 0, args.gpus) * 256 * 3 * 8,
                              "peer_pairs": pairs, "peer_access_enabled": enabled,

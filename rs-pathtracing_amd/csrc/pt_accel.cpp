@@ -205,41 +205,68 @@ struct Builder {
 
 }  // namespace
 
-// The quantized nodes of a large tree (DNodeQ): per axis the grid step is the smallest power of two with which
-// 65535 steps from g0 = floor(lo / step) * step cover the root box; every lo plane is rounded down to the grid
-// and every hi plane up, checked in f64 (g0 + q * step is exact there).  Left empty if a leaf's skip is not the
-// next node (the threaded layouts always make it so) or a link does not fit.
-void build_qnodes(Accel &a) {
-    const size_t per_oct = a.nodes.size() / BVH_OCTANTS;
+// The grid of the quantized nodes: per axis the step is the smallest power of two with which 65535 steps from
+// g0 = floor(lo / step) * step cover the root box.  False (grid unset) when the box is not finite or too wide for
+// a finite step.
+static bool make_grid(Accel &a) {
     double lo[3], hi[3];
     for (int k = 0; k < 3; k++) lo[k] = INFINITY, hi[k] = -INFINITY;
     for (const DNode &n : a.nodes)
         for (int k = 0; k < 3; k++) lo[k] = std::min(lo[k], n.lo[k]), hi[k] = std::max(hi[k], n.hi[k]);
     for (int k = 0; k < 3; k++) {
-        if (!(std::isfinite(lo[k]) && std::isfinite(hi[k]))) return;
+        if (!(std::isfinite(lo[k]) && std::isfinite(hi[k]) && std::isfinite(hi[k] - lo[k]))) return false;
         double step = std::ldexp(1.0, std::ilogb(std::max(hi[k] - lo[k], 1e-300) / 65535.0));
-        for (;;) {
+        for (int guard = 0;; guard++) {
             const double g0 = std::floor(lo[k] / step) * step;
-            if (std::ceil((hi[k] - g0) / step) <= 65535.0 && g0 <= lo[k]) {
+            if (std::isfinite(g0) && std::ceil((hi[k] - g0) / step) <= 65535.0 && g0 <= lo[k]) {
                 a.qg0[k] = g0;
                 a.qgs[k] = step;
                 break;
             }
             step *= 2.0;
+            if (!std::isfinite(step) || guard > 64) return false;
         }
     }
-    auto q_down = [&](double v, int k) {
-        double q = std::floor((v - a.qg0[k]) / a.qgs[k]);
-        while (q > 0 && a.qg0[k] + q * a.qgs[k] > v) q -= 1.0;
-        return std::max(0.0, std::min(65535.0, q));
-    };
-    auto q_up = [&](double v, int k) {
-        double q = std::ceil((v - a.qg0[k]) / a.qgs[k]);
-        while (q < 65535.0 && a.qg0[k] + q * a.qgs[k] < v) q += 1.0;
-        return std::max(0.0, std::min(65535.0, q));
-    };
+    return true;
+}
+// a plane rounded down (lo) or up (hi) to the grid, as a step count in [0, 65535]
+static double q_down(const Accel &a, double v, int k) {
+    double q = std::floor((v - a.qg0[k]) / a.qgs[k]);
+    while (q > 0 && a.qg0[k] + q * a.qgs[k] > v) q -= 1.0;
+    return std::max(0.0, std::min(65535.0, q));
+}
+static double q_up(const Accel &a, double v, int k) {
+    double q = std::ceil((v - a.qg0[k]) / a.qgs[k]);
+    while (q < 65535.0 && a.qg0[k] + q * a.qgs[k] < v) q += 1.0;
+    return std::max(0.0, std::min(65535.0, q));
+}
+
+// The quantized nodes of a large tree (DNodeQ) on the grid of make_grid: every lo plane is rounded down to the
+// grid and every hi plane up, checked in f64 (g0 + q * step is exact there).  Left empty if the grid cannot be
+// made, a leaf's skip is not the next node (the threaded layouts always make it so) or a link does not fit.
+// A one-shape leaf's link names its 64-byte record (DLeafRec, qleaves), laid out in octant 0's order so that
+// leaves of one subtree share lines.
+void build_qnodes(Accel &a, const Scene &sc) {
+    const size_t per_oct = a.nodes.size() / BVH_OCTANTS;
+    if (!make_grid(a)) return;
     std::vector<DNodeQ> out;
     out.reserve(a.nodes.size());
+    // the one-shape leaves' records in octant 0's order
+    std::vector<int32_t> rec_of(a.leaf.size() + 1, -1);  // by leaf-list index
+    std::vector<DLeafRec> recs;
+    for (size_t ni = 0; ni < per_oct; ni++) {
+        const DNode &n = a.nodes[ni];
+        if (n.count != 1 || !(a.cnodes[ni].first_count >> 31)) continue;
+        const int id = a.leaf[n.first];
+        const DShape d = to_device(sc.shapes[id]);
+        DLeafRec l{};
+        l.m[0] = d.inv[0], l.m[1] = d.inv[5], l.m[2] = d.inv[10];
+        l.m[3] = d.inv[3], l.m[4] = d.inv[7], l.m[5] = d.inv[11];
+        l.shape = id;
+        l.axis = d.axis;
+        rec_of[n.first] = (int32_t)recs.size();
+        recs.push_back(l);
+    }
     double bound = 0.0;
     for (int k = 0; k < 3; k++) bound = std::max(bound, std::fabs(a.qg0[k]));
     for (size_t ni = 0; ni < a.nodes.size(); ni++) {
@@ -247,7 +274,7 @@ void build_qnodes(Accel &a) {
         const int oct = (int)(ni / per_oct);
         DNodeQ c{};
         for (int k = 0; k < 3; k++) {
-            const double ql = q_down(n.lo[k], k), qh = q_up(n.hi[k], k);
+            const double ql = q_down(a, n.lo[k], k), qh = q_up(a, n.hi[k], k);
             if (a.qg0[k] + ql * a.qgs[k] > n.lo[k] || a.qg0[k] + qh * a.qgs[k] < n.hi[k]) return;  // (cannot happen)
             bound = std::max({bound, std::fabs(a.qg0[k] + ql * a.qgs[k]), std::fabs(a.qg0[k] + qh * a.qgs[k])});
             const bool neg = (oct >> k) & 1;  // the octant's rays move toward -k: hi is the near plane
@@ -261,11 +288,17 @@ void build_qnodes(Accel &a) {
             if ((size_t)n.skip != ni % per_oct + 1 || n.count > 63) return;
             const uint32_t fc = a.cnodes[ni].first_count;  // the compact form's leaf: direct id or list index
             const bool direct = fc >> 31;
-            c.link = 1u << 31 | (direct ? 1u << 30 : 0u) | (uint32_t)n.count << 24 | (fc & 0xffffffu);
+            uint32_t first = fc & 0xffffffu;
+            if (direct) {  // the record of the shape (octant 0 lists every leaf)
+                if (rec_of[n.first] < 0) return;
+                first = (uint32_t)rec_of[n.first];
+            }
+            c.link = 1u << 31 | (direct ? 1u << 30 : 0u) | (uint32_t)n.count << 24 | first;
         }
         out.push_back(c);
     }
     a.qnodes.swap(out);
+    a.qleaves.swap(recs);
     a.qbound = (float)bound;
     if ((double)a.qbound < bound) a.qbound = std::nextafter(a.qbound, INFINITY);
 }
@@ -338,7 +371,9 @@ Accel build_accel(const Scene &sc, int json_shapes, int leaf_max) {
             c.first_count = (uint32_t)n.first | (uint32_t)n.count << 24;
         a.cnodes.push_back(c);
     }
-    if (per_oct >= (size_t)BIG_BVH_NODES) build_qnodes(a);
+    if (per_oct >= (size_t)BIG_BVH_NODES) {
+        build_qnodes(a, sc);
+    }
     return a;
 }
 

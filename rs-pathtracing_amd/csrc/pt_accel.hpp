@@ -40,6 +40,8 @@ struct Accel {
     float bvh_bound = 0.f;  // >= |every plane of cnodes| (dev::Scene::bvh_bound)
     // the quantized nodes (trees of at least BIG_BVH_NODES nodes per layout; empty otherwise) and their grid
     std::vector<DNodeQ> qnodes;
+    // the one-shape leaves' records (DLeafRec, octant 0's order), which their quantized links name
+    std::vector<DLeafRec> qleaves;
     double qg0[3] = {0, 0, 0}, qgs[3] = {0, 0, 0};
     float qbound = 0.f;  // >= |every quantized plane| and >= |qg0|
 };
@@ -50,7 +52,8 @@ constexpr int LIN_MAX = 32;  // JSON shape count up to which the JSON shapes for
 Accel build_accel(const Scene &sc, int json_shapes, int leaf_max = 1);
 // the quantized nodes of a's layouts (build_accel does this for trees of at least BIG_BVH_NODES nodes per layout;
 // tests call it for smaller ones)
-void build_qnodes(Accel &a);
+void build_qnodes(Accel &a, const Scene &sc);
+
 // conservative world AABB of one shape (reference get_bounding_box + padding)
 DBox shape_box(const HostShape &s);
 

@@ -290,8 +290,8 @@ void free_share(GpuShare &g) {
     (void)hipSetDevice(g.device);
     if (g.stream) (void)hipStreamSynchronize(g.stream);
     DeviceScene &d = g.ds;
-    void *bufs[] = {d.shapes, d.mats, d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin, d.images,
-                    d.pixels, d.guard};
+    void *bufs[] = {d.shapes, d.mats, d.nodes, d.qnodes, d.leaf, d.lin, d.march, d.boxes, d.tex, d.perlin,
+                    d.images, d.pixels, d.guard};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     d = DeviceScene{};
@@ -355,11 +355,14 @@ int stage_accel(int device, const Accel &acc, StagedAccel *out, int *fault = nul
         g.bound = acc.qbound;
         const size_t nb = acc.qnodes.size() * sizeof(DNodeQ);
         if (fault && *fault > 0 && (*fault)-- == 1) err = hipErrorOutOfMemory;
-        // (one node of padding past the last layout: the walk may load node n + 1 ahead, PT_WALK_PREFETCH)
-        if (err == hipSuccess) err = hipMalloc((void **)&a.qnodes, sizeof(DQGrid) + nb + sizeof(DNodeQ));
+        // (one node of padding past the last layout, then the one-shape leaves' records: qleaf_offset)
+        const size_t ro = qleaf_offset(acc.nodes_per_octant()), rb = acc.qleaves.size() * sizeof(DLeafRec);
+        if (err == hipSuccess) err = hipMalloc((void **)&a.qnodes, ro + rb);
         if (err == hipSuccess) err = hipMemset((char *)(a.qnodes + 1) + nb, 0, sizeof(DNodeQ));
         if (err == hipSuccess) err = hipMemcpy(a.qnodes, &g, sizeof g, hipMemcpyHostToDevice);
         if (err == hipSuccess) err = hipMemcpy(a.qnodes + 1, acc.qnodes.data(), nb, hipMemcpyHostToDevice);
+        if (err == hipSuccess && rb)
+            err = hipMemcpy((char *)a.qnodes + ro, acc.qleaves.data(), rb, hipMemcpyHostToDevice);
     }
     if (err != hipSuccess) {
         free_staged(device, a);

@@ -14,6 +14,7 @@
 // count doubles, and a 64-bit FNV-1a checksum over everything before it taken
 // as 64-bit words (word-wise, so a 200 MB 4K frame checks at memory speed).
 #include <atomic>
+#include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -100,12 +101,17 @@ int pt_checkpoint_save(const char *path, const pt_checkpoint *c, const double *s
     std::string dir(path);
     const size_t slash = dir.find_last_of('/');
     dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : dir.substr(0, slash));
+    // The new file is in place from here on.  A file system that cannot sync a directory (EINVAL, ENOTSUP, e.g.
+    // some FUSE and network mounts) makes the rename as durable as it can be: that is success.  Any other failure
+    // is PT_ERR_IO, and the message says the checkpoint was written but its directory entry may not be durable.
     const int dfd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
-    if (dfd < 0 || ::fsync(dfd) != 0) {
-        if (dfd >= 0) ::close(dfd);
-        return ck_fail(PT_ERR_IO, "pt_checkpoint_save: cannot sync the directory of " + std::string(path));
-    }
+    if (dfd < 0) return PT_OK;  // (no directory handle to sync: the rename itself has completed)
+    const int rc = ::fsync(dfd);
+    const int err = errno;
     ::close(dfd);
+    if (rc != 0 && err != EINVAL && err != ENOTSUP && err != EOPNOTSUPP)
+        return ck_fail(PT_ERR_IO, "pt_checkpoint_save: " + std::string(path) +
+                                      " was written, but syncing its directory failed (the rename may not be durable)");
     return PT_OK;
 }
 

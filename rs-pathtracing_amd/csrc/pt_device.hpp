@@ -392,6 +392,14 @@ PT_HD bool wave_all(bool p) {
     return p;
 #endif
 }
+// A leaf record's sphere with a diagonal inverse transform (DLeafRec::axis): sphere_axis_t on the record's six
+// entries, the same operations on the same values.
+PT_HD bool sphere_axis_rec(const double *m, V3 ro, V3 rd, double min_t, double max_t, double *t) {
+    const V3 o = v3(ro.x * m[0] + m[3], ro.y * m[1] + m[4], ro.z * m[2] + m[5]);
+    const V3 d = v3(rd.x * m[0], rd.y * m[1], rd.z * m[2]);
+    return sphere_t(o, d, min_t, max_t, t);
+}
+
 // One leaf of the BVH (a shape id, or `count` ids from leaf[first]) against (best, who), with the tie rule.
 template <bool STATS>
 PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first, int count, bool direct,
@@ -552,7 +560,24 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
                 PT_LP(BVH_ENTER);
                 if (link >> 31) {  // a leaf
                     const int first = (int)(link & 0xffffffu), count = (int)(link >> 24 & 0x3fu);
-                    bvh_leaf_test<STATS>(sc, r, axis_ok, first, count, (link >> 30) & 1u, min_t, best, who, ct);
+                    if ((link >> 30) & 1u) {  // a one-shape leaf's 64-byte record
+                        const DLeafRec &L = ((const DLeafRec *)((const char *)sc.qnodes + qleaf_offset(sc.nnodes)))[first];
+                        const int i = L.shape;
+                        double t;
+                        bool h;
+                        if (axis_ok && L.axis) {
+                            if (STATS) ct->c[C_TEST_SPHERE]++;
+                            h = sphere_axis_rec(L.m, r.o, r.d, min_t, best, &t);
+                        } else {
+                            h = shape_test<STATS, march::F_ANY, false>(sc.shapes[i], r, min_t, best, &t, ct);
+                        }
+                        if (h && (t < best || i > who)) {
+                            best = t;
+                            who = i;
+                        }
+                    } else {
+                        bvh_leaf_test<STATS>(sc, r, axis_ok, first, count, (link >> 30) & 1u, min_t, best, who, ct);
+                    }
                     best32 = (float)(best + fabs(best) * 0x1p-20);
                 }
                 n++;

@@ -93,6 +93,10 @@ struct alignas(16) DNodeQ {
     uint32_t link;
 };
 static_assert(sizeof(DNodeQ) == 16, "DNodeQ is a quarter cache line");
+// byte offset of the leaf records in the quantized nodes' buffer (grid, layouts, one node of padding, records)
+__host__ __device__ inline size_t qleaf_offset(int nnodes_per_octant) {
+    return 64 + ((size_t)(8 * (size_t)nnodes_per_octant + 1) * 16 + 63) / 64 * 64;
+}
 // The quantized nodes' device buffer starts with their grid; the octant layouts follow it.
 struct alignas(64) DQGrid {
     double g0[3], gs[3];
@@ -102,6 +106,18 @@ struct alignas(64) DQGrid {
 static_assert(sizeof(DQGrid) == 64, "DQGrid is one cache line");
 
 constexpr int BIG_BVH_NODES = 1 << 15;  // binary nodes from which the bounce runs its large-tree builds (C5)
+
+// A one-shape leaf of the large-tree walk's quantized nodes (round 6): the shape id, and for a sphere whose inverse
+// transform is a diagonal scale plus a translation (DShape::axis) the six entries sphere_axis_t reads (m0, m5,
+// m10, m3, m7, m11), so its exact test reads this 64-byte record (one line, siblings' records adjacent) and not
+// two lines of the 320-byte shape; any other shape is tested from sc.shapes.  C5 walk 179.5 -> 172.0 ms per
+// one-stream frame, 2118 -> 2180 M samples/s (profiles/r6/ab/r6c_wide_dp_qrec_c5.log).
+struct alignas(64) DLeafRec {
+    double m[6];
+    int32_t shape, axis;
+    int32_t pad[2];
+};
+static_assert(sizeof(DLeafRec) == 64, "DLeafRec is one 64-byte record");
 
 struct DBox {
     double lo[3], hi[3];

@@ -1510,60 +1510,86 @@ template <int NW>
 static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws, int fkind) {
     const Tuning &tu = ws->tune;
-    // path slots per chunk: Tuning::wf_paths, or by depth (deep frames: bigger chunks, fewer tails)
-    const uint32_t cap_want = tu.wf_paths ? (uint32_t)tu.wf_paths : (P0.depth > 16 ? 1u << 27 : 3u << 24);
     // the launch's samples: the frame's, or a resumable frame's window [s_begin, s_end) of them
     const uint32_t s_begin = P0.s_begin, s_end = P0.s_end ? P0.s_end : P0.spp, nsw = s_end - s_begin;
-    // tile groups (only for frames beyond cap_want pixels), then sample chunks
-    const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
     const uint32_t ntiles = P0.tile_count;
-    const uint32_t group_tiles = ntiles < tiles_per_group ? ntiles : tiles_per_group;
-    const uint32_t npix_max = group_tiles * TILE * TILE;
-    uint32_t ns = cap_want / npix_max;
-    if (ns < 1) ns = 1;
-    if (ns > nsw) ns = nsw;
-    {
-        // A small frame (one rank's share of a multi-GPU frame) still gets at
-        // least wf_min_chunks sample chunks, so the pipelined slots overlap one
-        // chunk's short tail iterations with the next chunk's work; chunks
-        // keep at least MIN_CHUNK_PATHS paths to fill the device.
-        // (a progressive frame's band, P0.stop set, gets at least two: one per chunk stream; and any frame at
-        // least one per chunk stream while its chunks keep MIN_CHUNK_PATHS paths, whatever wf_paths allows)
+    const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
+    const size_t cnt_words = (size_t)(iters + 2) * 4;
+    auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+    // pre-selected march jobs (one marched shape): the bounce kernel hands the march its object-space ray
+    // and bound (C2 +9 %: iso march 340 -> 275 ms, bounce 248 -> 256, round 1)
+    const bool presel = sc.nmarch == 1 && !ws->diag;
+    // The chunk plan for cap_want path slots per chunk: tile groups (only for frames beyond cap_want pixels),
+    // then sample chunks, the streams, and the workspace bytes.
+    struct Plan {
+        uint32_t group_tiles, npix_max, ns, cap, cap_tiles;
+        int slots;
+        size_t att_bytes, slot_bytes, bytes;
+    };
+    auto plan_for = [&](uint32_t cap_want) {
+        Plan pl;
+        const uint32_t tiles_per_group = cap_want / (TILE * TILE) ? cap_want / (TILE * TILE) : 1;
+        pl.group_tiles = ntiles < tiles_per_group ? ntiles : tiles_per_group;
+        pl.npix_max = pl.group_tiles * TILE * TILE;
+        uint32_t ns = cap_want / pl.npix_max;
+        if (ns < 1) ns = 1;
+        if (ns > nsw) ns = nsw;
+        // A small frame (one rank's share of a multi-GPU frame) still gets at least wf_min_chunks sample
+        // chunks, so the pipelined slots overlap one chunk's short tail iterations with the next chunk's work;
+        // chunks keep at least MIN_CHUNK_PATHS paths to fill the device.  (A progressive frame's band, P0.stop
+        // set, gets at least two: one per chunk stream; and any frame at least one per chunk stream while its
+        // chunks keep MIN_CHUNK_PATHS paths, whatever wf_paths allows.)
         uint32_t mc = P0.stop && tu.wf_min_chunks < 2 ? 2u : (uint32_t)tu.wf_min_chunks;
         if (mc < (uint32_t)tu.wf_slots) mc = (uint32_t)tu.wf_slots;
-        if (mc > 1 && ntiles <= group_tiles) {
+        if (mc > 1 && ntiles <= pl.group_tiles) {
             uint32_t want = (nsw + mc - 1) / mc;
-            const uint32_t floor_ns = (MIN_CHUNK_PATHS + npix_max - 1) / npix_max;
+            const uint32_t floor_ns = (MIN_CHUNK_PATHS + pl.npix_max - 1) / pl.npix_max;
             if (want < floor_ns) want = floor_ns;
             if (want < ns) ns = want;
         }
+        pl.ns = ns;
+        pl.cap = ns * pl.npix_max;
+        pl.cap_tiles = (pl.cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
+        // no more slots than chunks
+        const uint64_t chunks = (uint64_t)((ntiles + pl.group_tiles - 1) / pl.group_tiles) * ((nsw + ns - 1) / ns);
+        pl.slots = tu.wf_slots;
+        if ((uint64_t)pl.slots > chunks) pl.slots = (int)chunks;
+        const size_t cap = pl.cap;
+        pl.att_bytes = sc.tex ? cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
+        // two path-state sets, leaf records, lists, id stacks, statuses, compaction tiles, counters
+        pl.slot_bytes = al(cap * PathSoA::BYTES) * 2 + al(cap * 32) + (presel ? al(cap * 64) : 0) + al(cap * 4) * 2 +
+                        al(cap * 4 * (P0.depth + 1)) + al((size_t)pl.cap_tiles * CP_TILE) +
+                        al(((size_t)pl.cap_tiles + CP_BLOCK) * 12) + al(cnt_words * 4) + al(pl.att_bytes);
+        pl.bytes = pl.slot_bytes * (size_t)pl.slots + al((size_t)pl.npix_max * 24) + 8192;
+        return pl;
+    };
+    // Path slots per chunk: Tuning::wf_paths, or by depth (deep frames: bigger chunks, fewer tails), halved
+    // until the plan fits the device memory the workspace may take (what is free plus what it holds now, less
+    // 2 GiB): a deep textured frame's per-slot attenuation values ((depth + 1) * 24 B per path) would otherwise
+    // ask for more than the device has (1080p, 256 spp, depth 50 at 128M paths needed ~430 GB).
+    uint32_t cap_want = tu.wf_paths ? (uint32_t)tu.wf_paths : (P0.depth > 16 ? 1u << 27 : 3u << 24);
+    Plan pl = plan_for(cap_want);
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            const size_t reserve_b = (size_t)2 << 30;
+            const size_t avail = free_b + ws->bytes > reserve_b ? free_b + ws->bytes - reserve_b : 0;
+            while (pl.bytes > avail && cap_want > MIN_CHUNK_PATHS) {
+                cap_want = cap_want / 2 > MIN_CHUNK_PATHS ? cap_want / 2 : MIN_CHUNK_PATHS;
+                pl = plan_for(cap_want);
+            }
+        }
     }
-    const uint32_t cap = ns * npix_max;
-    const int iters = (int)P0.depth + 2;  // traces per path <= depth + 1, then one last shade
-    const size_t cnt_words = (size_t)(iters + 2) * 4;
-    const uint32_t cap_tiles = (cap + CP_TILE - 1) / CP_TILE;  // compaction tiles (status padded to them)
-    // no more slots than chunks
-    const uint64_t chunks = (uint64_t)((ntiles + group_tiles - 1) / group_tiles) * ((nsw + ns - 1) / ns);
-    int slots = tu.wf_slots;
-    if ((uint64_t)slots > chunks) slots = (int)chunks;
+    const uint32_t group_tiles = pl.group_tiles, npix_max = pl.npix_max, ns = pl.ns, cap = pl.cap,
+                   cap_tiles = pl.cap_tiles;
+    const int slots = pl.slots;
+    const size_t att_bytes = pl.att_bytes, bytes = pl.bytes;
     hipError_t e = ensure_streams(ws, slots);
     if (e != hipSuccess) return e;
     // One workspace serves every frame of the renderer, whichever stream it is
     // queued on (render_start's own stream, a caller's stream in
     // render_device): this frame's kernels wait for the previous frame's.
     if (ws->used && (e = hipStreamWaitEvent(st, ws->done, 0)) != hipSuccess) return e;
-    auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
-    const size_t att_bytes = sc.tex ? (size_t)cap * 24 * (P0.depth + 1) : 0;  // textured attenuation values
-    // pre-selected march jobs (one marched shape): the bounce kernel hands the march its object-space ray
-    // and bound (C2 +9 %: iso march 340 -> 275 ms, bounce 248 -> 256, round 1)
-    const bool presel = sc.nmarch == 1 && !ws->diag;
-    // two path-state sets (8 + 3 words per path each), leaf records, lists
-    const size_t slot_bytes = al((size_t)cap * PathSoA::BYTES) * 2 + al((size_t)cap * 32) +
-                              (presel ? al((size_t)cap * 64) : 0) + al((size_t)cap * 4) * 2 +
-                              al((size_t)cap * 4 * (P0.depth + 1)) +
-                              al((size_t)cap_tiles * CP_TILE) + al(((size_t)cap_tiles + CP_BLOCK) * 12) + al(cnt_words * 4) +
-                              al(att_bytes);
-    const size_t bytes = slot_bytes * (size_t)slots + al((size_t)npix_max * 24) + 8192;
     e = reserve(ws, bytes);
     if (e != hipSuccess) return e;
     // carve the workspace: the slots' path state, then the shared running sums

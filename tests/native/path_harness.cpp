@@ -42,10 +42,12 @@ extern "C" void *h_scene_new(const char *json, size_t len, int random_spheres, u
         b->view.perlin = tex ? b->sc.perlins.data() : nullptr;
         b->view.images = tex ? b->sc.images.data() : nullptr;
         b->view.pixels = tex ? b->sc.pixels.data() : nullptr;
-        if (b->acc.qnodes.empty() && !b->acc.nodes.empty()) build_qnodes(b->acc);  // (small trees too)
+        if (b->acc.qnodes.empty() && !b->acc.nodes.empty()) build_qnodes(b->acc, b->sc);  // (small trees too)
         if (!b->acc.qnodes.empty()) {
             const size_t nb = b->acc.qnodes.size() * sizeof(DNodeQ);
-            b->qbuf.resize(2 + (nb + sizeof(DQGrid) - 1) / sizeof(DQGrid));  // (+ padding past the layouts)
+            const size_t ro = qleaf_offset(b->acc.nodes_per_octant()), rb = b->acc.qleaves.size() * sizeof(DLeafRec);
+            b->qbuf.resize((ro + rb + sizeof(DQGrid) - 1) / sizeof(DQGrid) + 1);  // (+ padding, the leaf records)
+            if (rb) std::memcpy((char *)b->qbuf.data() + ro, b->acc.qleaves.data(), rb);
             DQGrid &g = b->qbuf[0];
             for (int k = 0; k < 3; k++) g.g0[k] = b->acc.qg0[k], g.gs[k] = b->acc.qgs[k];
             g.bound = b->acc.qbound;
@@ -126,7 +128,17 @@ extern "C" int h_qnode_check(void *p) {
             ok = ok && !(l >> 31) && (int32_t)l == N[i].skip;
         } else {
             const uint32_t fc = Cn[i].first_count;
-            ok = ok && (l >> 31) && (int)(l >> 24 & 0x3fu) == N[i].count && (l & 0xffffffu) == (fc & 0xffffffu) &&
+            const bool rec = (l >> 30) & 1u;  // a one-shape leaf's record names the shape
+            const uint32_t named = rec ? ((l & 0xffffffu) < b->acc.qleaves.size()
+                                              ? (uint32_t)b->acc.qleaves[l & 0xffffffu].shape : ~0u)
+                                       : (l & 0xffffffu);
+            if (rec && named != ~0u) {  // the record's axis entries are its shape's
+                const DLeafRec &L = b->acc.qleaves[l & 0xffffffu];
+                const DShape &S = b->shapes[named];
+                ok = ok && L.axis == S.axis && L.m[0] == S.inv[0] && L.m[1] == S.inv[5] && L.m[2] == S.inv[10] &&
+                     L.m[3] == S.inv[3] && L.m[4] == S.inv[7] && L.m[5] == S.inv[11];
+            }
+            ok = ok && (l >> 31) && (int)(l >> 24 & 0x3fu) == N[i].count && named == (fc & 0xffffffu) &&
                  ((l >> 30) & 1u) == (fc >> 31) && (size_t)N[i].skip == i % per + 1;
         }
         bad += !ok;

@@ -40,9 +40,58 @@ def test_device_shortfall():
 def test_plain_multi_gpu_bench_refuses_too_few_devices():
     """On this CPU container no device is visible: a plain --gpus 2 over nccl exits non-zero at once, naming the
     device count, before any rank starts."""
+    # (no device visible to the child whatever the host has: it must refuse, not start a real 2-rank bench)
+    env = {k: v for k, v in __import__("os").environ.items() if k != "WORLD_SIZE"}
+    env.update(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"],
-                       capture_output=True, text=True, timeout=300, cwd=str(ROOT),
-                       env={k: v for k, v in __import__("os").environ.items() if k != "WORLD_SIZE"})
+                       capture_output=True, text=True, timeout=300, cwd=str(ROOT), env=env)
     assert r.returncode == 2, r.stderr[-2000:]
     assert "need 2 GPUs" in r.stderr and "0 devices are visible" in r.stderr
     assert "launching" not in r.stderr
+
+
+def test_topology_fields_and_refusal():
+    """A multi-rank line reports what each rank ran on; under nccl two ranks on one physical GPU are refused
+    (the line would not measure N GPUs), under gloo (a rehearsal on fewer GPUs) they are reported, not refused."""
+    dev = lambda r, u: {"rank": r, "local_rank": r, "device": r, "pci": "0000:%02x:00" % (0x10 + u), "uuid": "GPU-%d" % u,
+                        "name": "AMD Instinct MI355X"}
+    ok = bench.device_topology([dev(1, 1), dev(0, 0)], "nccl", 2)
+    assert ok["distinct_devices"] == 2 and ok["shared_devices"] == [] and ok["comm_size"] == 2
+    assert [i["rank"] for i in ok["ranks"]] == [0, 1] and ok["backend"] == "nccl"
+    assert bench.topology_refusal(ok) is None
+    same = bench.device_topology([dev(0, 0), dev(1, 0), dev(2, 1)], "nccl", 3)
+    assert same["shared_devices"] == [[0, 1]] and same["distinct_devices"] == 2
+    msg = bench.topology_refusal(same)
+    assert msg and "share a device" in msg and "[[0, 1]]" in msg
+    rehearsal = bench.device_topology([dev(0, 0), dev(1, 0)], "gloo", 2)
+    assert rehearsal["shared_devices"] == [[0, 1]] and bench.topology_refusal(rehearsal) is None
+    assert "communicator size" in bench.topology_refusal(bench.device_topology([dev(0, 0)], "gloo", 2))
+
+
+def _gather_identities(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = {"rank": rank, "local_rank": rank, "device": 0, "pci": "0000:%02x:00" % rank, "uuid": "GPU-%d" % rank,
+            "name": "x"}
+    infos = [None] * world
+    dist.all_gather_object(infos, mine)
+    topo = bench.device_topology(infos, "nccl", dist.get_world_size())
+    out.put((rank, topo["distinct_devices"], topo["comm_size"], bench.topology_refusal(topo)))
+    dist.destroy_process_group()
+
+
+def test_topology_gathered_over_two_ranks():
+    """The identities go through the same all_gather_object bench.py uses (gloo, world 2, CPU)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_gather_identities, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == [(0, 2, 2, None), (1, 2, 2, None)]

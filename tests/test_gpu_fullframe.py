@@ -105,6 +105,19 @@ def test_c5_full_frame_every_pixel(pt):
     _every_pixel(img, ref)
 
 
+def test_c1_full_frame_every_pixel(pt, spheres_text):
+    """C1 at its own size (BASELINE configs[0]: spheres.json 256x256, 16 spp, depth 8, the bench's scene seed 1):
+    the frame through the C-ABI renderer against the oracle's linear scan with the literal march, every pixel
+    (1,048,576 samples, two marched Hearts)."""
+    w, h, spp, depth, seed = 256, 256, 16, 8, 1
+    ps = pt.Scene.from_json(spheres_text, seed=1)
+    r = pt.HipRenderer(ps, depth=depth)
+    img = r.render(ps.camera(), pt.ImageParams(w, h), spp, seed=seed)
+    ref = O.Scene(spheres_text, seed=1).render(w, h, spp, depth, seed, threads=host_threads())
+    _every_pixel(img, ref)
+    assert img.mean() > 0.05  # not a black frame
+
+
 def _compare_hits(got, osc, rays):
     bad = []
     for i, ray in enumerate(rays):

@@ -423,6 +423,29 @@ def test_textured_frames(pt, name, seed, depth, monkeypatch):
     assert img.mean() > 0.05
 
 
+def test_textured_deep_frame_fits_device_memory(pt, monkeypatch):
+    """A textured scene at the reference GUI's depth 50, 1920x1080, 128 spp: each path slot carries
+    (depth + 1) * 24 B of textured attenuation values, so the by-depth 128M-path chunk would need ~430 GB for two
+    chunk streams; the engine sizes its chunks to the device memory instead and the frame renders.  A sample of
+    pixels is checked against the oracle at the texture tolerance."""
+    import torch
+    from conftest import ROOT, host_threads, scene_text
+    monkeypatch.chdir(ROOT)
+    text = scene_text("textured.json")
+    w, h, spp, depth, seed = 1920, 1080, 128, 50, 5
+    ps, osc = pt.Scene.from_json(text, seed=1), O.Scene(text, seed=1)
+    r = pt.HipRenderer(ps, depth=depth)
+    frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    r.render_device(ps.camera(), w, h, spp, seed, 0, 1, frame.data_ptr(), stream)
+    torch.cuda.synchronize()
+    img = frame.view(-1, 3).cpu().numpy()
+    assert np.all(np.isfinite(img)) and img.mean() > 0.05
+    px = np.random.default_rng(12).choice(w * h, size=96, replace=False).astype(np.uint32)
+    ref = osc.render(w, h, spp, depth, seed, pixels=px, threads=host_threads())
+    check_image_tol(img[px], ref)
+
+
 def check_image_tol(img, ref):
     assert np.all(np.isfinite(img))
     assert np.all(rms(img, ref) <= RMS_TOL), rms(img, ref)

@@ -262,7 +262,8 @@ def test_bvh_fma_slab_build_same_hits(H):
 
 def test_quantized_nodes_contain_the_boxes(H):
     """The 16-byte nodes of the large-tree walk (DNodeQ): every box on the per-axis grid contains the node's f64
-    box (lo rounded down, hi up), interior links are the skips and leaf links decode to the leaf's shapes."""
+    box (lo rounded down, hi up), interior links are the skips and leaf links decode to the leaf's shapes (a
+    one-shape leaf through its 64-byte record, whose axis entries are the shape's)."""
     import sys
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
     import make_scenes
@@ -350,3 +351,4 @@ def test_large_tree_walk_far_origins_and_grazing_rays(H):
         assert (w0, t0.value) == (w1, t1.value) == (w2, t2.value), (o, d)
         hits += w0 >= 0
     assert hits > 500
+

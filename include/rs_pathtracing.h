@@ -165,9 +165,11 @@ int pt_renderer_peer_access(const pt_renderer *r, int *pairs, int *enabled);
 /* Tuning knobs of the render engines (not part of the reference; defaults are
  * the measured optimum): "engine" (0 auto, 1 megakernel,
  * 2 wavefront), "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
- * "wf_bounce_waves", "wf_march_slice", "wf_march_blocks_per_cu",
- * "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "wf_walk", "bvh_leaf" (shapes
- * per BVH leaf: setting it rebuilds the BVH on every device).  A new renderer
+ * "wf_bounce_waves", "wf_march_slice", "wf_walk", "bvh_leaf" (shapes per BVH
+ * leaf: setting it rebuilds the BVH on every device).  (ABI 4's
+ * "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "wf_stagger"
+ * and "wf_tail_paths" were measured slower and removed; setting one is
+ * PT_ERR_INVALID.)  A new renderer
  * starts from the defaults; set_option changes them for every device of the
  * renderer (not while a render_start frame is in flight).  No knob changes the
  * image: every setting renders the same bits.  pt_option_name(i) lists the
@@ -334,8 +336,8 @@ int pt_render_stop_stats(pt_renderer *r, uint64_t *skipped, uint64_t *worked);
 /* Per-kernel launch timing of the render path (bench / roofline): returns
  * the summed HIP-event durations (ms) and launch counts per kernel kind since
  * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
- * reduce, [4] megakernel, [5] wavefront tail (wf_tail: a chunk's last live
- * paths run to their ends), [6] BVH walk (wf_walk) — into ms[nkinds] / launches[nkinds] (either may be
+ * reduce, [4] megakernel, [5] unused (always 0; was the wavefront tail kernel,
+ * removed), [6] BVH walk (wf_walk) — into ms[nkinds] / launches[nkinds] (either may be
  * NULL), then turns recording on (enable = 1) or off.  Events are recorded on
  * the stream each kernel is launched on.  PT_ERR_STATE while a render_start
  * frame is in flight (its band feeder records into the same timer). */

@@ -498,7 +498,8 @@ def march_jobs(renderer: "HipRenderer", jobs, status=False):
     return (t, st, it) if status else (t, st == 1, it)
 
 
-KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", "tail", "walk"]
+# (slot 5 was the wavefront tail kernel, removed in round 6: always 0, not reported)
+KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", None, "walk"]
 
 
 def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
@@ -507,7 +508,7 @@ def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:
     ms = (C.c_double * len(KERNEL_KINDS))()
     n = (C.c_uint32 * len(KERNEL_KINDS))()
     _check(lib().pt_kernel_timing(renderer._h, 1 if enable else 0, ms, n, len(KERNEL_KINDS)))
-    return {k: (ms[i], n[i]) for i, k in enumerate(KERNEL_KINDS)}
+    return {k: (ms[i], n[i]) for i, k in enumerate(KERNEL_KINDS) if k}
 
 
 def wave_diag(renderer: "HipRenderer", enable: bool = True):
@@ -540,9 +541,7 @@ def option_names() -> list:
 
 # the defaults (pt_kernel.hpp Tuning): bench.py reports knobs that differ
 OPTION_DEFAULTS = {"engine": 0, "mega_waves": 4, "diag": 0, "wf_slots": 2, "wf_paths": 0, "wf_min_chunks": 1,
-                   "wf_bounce_waves": 3, "wf_march_slice": 256,
-                   "wf_march_blocks_per_cu": 0, "wf_side_priority": 0,
-                   "wf_pingpong": 0, "wf_stagger": 0, "wf_tail_paths": 0, "wf_walk": 5, "bvh_leaf": 1}
+                   "wf_bounce_waves": 3, "wf_march_slice": 256, "wf_walk": 5, "bvh_leaf": 1}
 
 
 def shard_tiles(width: int, height: int, rank: int, world: int) -> int:

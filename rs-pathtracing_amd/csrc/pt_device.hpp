@@ -92,20 +92,8 @@ PT_HD V3 xf_normal(const double *m, V3 n) {
               n.x * m[2] + n.y * m[6] + n.z * m[10]);
 }
 
-#ifndef PT_SLAB32
-#define PT_SLAB32 1  // the large-tree builds' BVH slab test in f32 with a conservative widening (C5 +1.3 %, r4f)
-#endif
-#ifndef PT_RECT_SIGN
-#define PT_RECT_SIGN 0  // rectangles: rays moving away from the plane rejected before the division (round 5 A/B: C2 2061 -> 2034, off)
-#endif
-#ifndef PT_WALK_PREFETCH
-#define PT_WALK_PREFETCH 0  // the quantized walk loads node n + 1 with node n
-#endif
-#ifndef PT_AXIS_LEAF
-#define PT_AXIS_LEAF 2  // BVH leaf spheres with a diagonal inverse transform take sphere_axis_t: 1 in every build,
-                        // 2 in the large-tree (FMA_SLAB) builds only (C5 +3.2 %; in the C2 bounce the extra path
-                        // costs 9 %: round-4 A/B r4g)
-#endif
+// (Measured and removed in round 6: the rectangles' rejection of rays moving away from the plane before the
+// division, C2 2061 -> 2034; the quantized walk loading node n + 1 with node n, C5 2112 -> 2035.)
 
 // ------------------------------------------------------------ primitives
 // Each returns true and sets *t on a hit in [min_t, max_t], object space.
@@ -232,10 +220,6 @@ PT_HD bool shape_test(const DShape &s, const Ray &r, double min_t, double max_t,
         const double *m = s.inv;
         const double oz = r.o.x * m[8] + r.o.y * m[9] + r.o.z * m[10] + m[11];
         const double dz = r.d.x * m[8] + r.d.y * m[9] + r.d.z * m[10];
-        // a ray moving away from the plane (oz, dz of one sign, or oz = 0) has t = -oz / dz <= 0, below a
-        // positive min_t: rejected without the division (NaN and dz = 0, the range test's quirk, go on)
-        if (PT_RECT_SIGN && min_t > 0.0 && dz != 0.0 && dz == dz && oz == oz && (oz == 0.0 || (oz < 0.0) == (dz < 0.0)))
-            return false;
         const double tt = -oz / dz;
         if (tt < min_t || tt > max_t) return false;
         PT_LP(RECT_ROWS);
@@ -358,7 +342,7 @@ struct Scene {
     int nnodes, nlin, nmarch, diag;  // diag bit 0: skip marched shapes (timing ablation only)
     int nmats;
     int ext;  // the scene needs the extended (EXT) builds: non-solid textures or a Torus
-    float bvh_bound;  // >= |every BVH node plane| (the f32 slab's error bound, PT_SLAB32)
+    float bvh_bound;  // >= |every BVH node plane| (the f32 slab's error bound)
     // marches dropped by the march guard (pt_march.hpp MARCH_GUARD), counted
     // on the device (pt_march_guard_drops); null: not counted
     unsigned long long *guard;
@@ -410,7 +394,7 @@ PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first,
         double t;
         const DShape &S = sc.shapes[i];
         bool h;
-        if (PT_AXIS_LEAF && axis_ok && S.axis) {
+        if (axis_ok && S.axis) {
             if (STATS) ct->c[C_TEST_SPHERE]++;
             h = sphere_axis_t(S.inv, r.o, r.d, min_t, best, &t);
         } else {
@@ -423,11 +407,10 @@ PT_HD void bvh_leaf_test(const Scene &sc, const Ray &r, bool axis_ok, int first,
     }
 }
 
-// QN (with FMA_SLAB and PT_SLAB32; sc.qnodes set): the BVH walk reads the quantized nodes (DNodeQ), 16 bytes
+// QN (with FMA_SLAB; sc.qnodes set): the BVH walk reads the quantized nodes (DNodeQ), 16 bytes
 // instead of 32: t = fma(q, gs / d, (g0 - o) / d -/+ e') per plane, the same culling with the grid folded into
 // the per-ray offsets and a wider margin (below).
-// PART: bit 0 the uniform list, bit 1 the BVH (PT_WALK_ULIST_IN_BOUNCE: the split bounce traces the uniform list,
-// wf_walk the BVH).
+// PART: bit 0 the uniform list, bit 1 the BVH.
 template <bool STATS = false, bool EXT = false, bool FMA_SLAB = false, bool QN = false, int PART = 3>
 PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, double *best_t, int *who_out,
                            Ctr *ct = nullptr, bool any = false) {
@@ -481,8 +464,10 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     auto tx = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.x, mx) : ((double)b - r.o.x) * inv.x; };
     auto ty = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.y, my) : ((double)b - r.o.y) * inv.y; };
     auto tz = [&](float b) { return FMA_SLAB ? __builtin_fma((double)b, inv.z, mz) : ((double)b - r.o.z) * inv.z; };
-    const bool axis_ok = (PT_AXIS_LEAF == 1 || (PT_AXIS_LEAF == 2 && FMA_SLAB)) && axis_ray_ok(r.o, r.d);
-    // SLAB32 (PT_SLAB32, the FMA_SLAB builds): the planes' t in f32, t = fma(b, 1/d, lo) for near planes and
+    // Axis-aligned sphere leaves (DShape::axis) take sphere_axis_t in the large-tree (FMA_SLAB) builds only (C5
+    // +3.2 %; in the C2 bounce build the extra path costs 9 % through register allocation: round-4 A/B r4g)
+    const bool axis_ok = FMA_SLAB && axis_ray_ok(r.o, r.d);
+    // SLAB32 (the FMA_SLAB builds; C5 +1.3 %, r4f): the planes' t in f32, t = fma(b, 1/d, lo) for near planes and
     // fma(b, 1/d, hi) for far ones, lo / hi = fl32(-o/d -/+ e), the widening e = 2^-21 (B + |o|) |1/d| (B >= every
     // plane's |b|) folded into the offset in f64: against the real t = (b - o) / d, the f32 1/d and lo / hi
     // (each one f32 rounding of the f64 value: 2^-24 relative) and the fma's rounding add up to less than
@@ -492,7 +477,7 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     // 1/d or -o/d does not fit an f32 is left open (NaN t's drop out of fmax/fmin), and so is one whose |1/d| is
     // below 1e-30, where an f32 flush of b * 1/d could exceed the widening; min_t is rounded down and best up.
     // The hits are decided by the exact f64 leaf tests as in every walk.
-    constexpr bool S32 = FMA_SLAB && PT_SLAB32;
+    constexpr bool S32 = FMA_SLAB;
     constexpr bool Q = S32 && QN;
     auto axis32 = [&](double o, double iv, float *i32, float *lo32, float *hi32) {
         const double m = -(o * iv);
@@ -543,12 +528,8 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
     if (!(PART & 2)) n = sc.nnodes;
     if (Q) {  // the quantized layouts
         const DNodeQ *qn = (const DNodeQ *)(sc.qnodes + 1) + (size_t)oct * (size_t)sc.nnodes;
-        // PT_WALK_PREFETCH: node n + 1 (where an entered node leads) is loaded with node n, so a descent's next
-        // node is in flight while this one is tested (the buffer holds one node of padding past the layouts)
-        uint4 raw_next = PT_WALK_PREFETCH && n < sc.nnodes ? *(const uint4 *)(qn + n) : make_uint4(0, 0, 0, 0);
         while (n < sc.nnodes) {
-            const uint4 raw = PT_WALK_PREFETCH ? raw_next : *(const uint4 *)(qn + n);
-            if (PT_WALK_PREFETCH) raw_next = *(const uint4 *)(qn + n + 1);
+            const uint4 raw = *(const uint4 *)(qn + n);
             PT_LP(BVH_NODE);
             if (STATS) ct->c[C_NODE_SLABS]++;
             const f2v a = __builtin_elementwise_fma((f2v){(float)(raw.x & 0xffffu), (float)(raw.x >> 16)}, pa_i, pa_m);
@@ -583,7 +564,6 @@ PT_HD void closest_nomarch(const Scene &sc, const Ray &r, V3 inv, double min_t, 
                 n++;
             } else {
                 n = (link >> 31) ? n + 1 : (int)link;  // a leaf's skip is the next node
-                if (PT_WALK_PREFETCH && !(link >> 31) && n < sc.nnodes) raw_next = *(const uint4 *)(qn + n);
             }
         }
     }

@@ -14,9 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 
-#ifndef PT_DEFAULT_WAVES
-#define PT_DEFAULT_WAVES 4  // C5 (100k spheres, compact BVH): 2 waves 845-849, 3: 1044, 4: 1109 M samples/s
-#endif
+constexpr int DEFAULT_WAVES = 4;  // C5 (100k spheres, compact BVH): 2 waves 845-849, 3: 1044, 4: 1109 M samples/s
 
 namespace pt {
 
@@ -278,8 +276,7 @@ static dev::Scene dscene(const DeviceScene &s) {
 
 // ------------------------------------------------------------- tuning
 const char *const TUNING_NAMES[] = {"engine", "mega_waves", "diag", "wf_slots", "wf_paths", "wf_min_chunks",
-                                    "wf_bounce_waves", "wf_march_slice",
-                                    "wf_march_blocks_per_cu", "wf_side_priority", "wf_pingpong", "wf_stagger", "wf_tail_paths", "wf_walk", "bvh_leaf", nullptr};
+                                    "wf_bounce_waves", "wf_march_slice", "wf_walk", "bvh_leaf", nullptr};
 
 static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *hi, int **iv) {
     struct F {
@@ -295,10 +292,6 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         {"wf_min_chunks", &Tuning::wf_min_chunks, 1, 4096},
         {"wf_bounce_waves", &Tuning::wf_bounce_waves, 2, 8},
         {"wf_march_slice", &Tuning::wf_march_slice, 0, 1 << 20},
-        {"wf_march_blocks_per_cu", &Tuning::wf_march_blocks_per_cu, 0, 64},
-        {"wf_side_priority", &Tuning::wf_side_priority, -1, 1},
-        {"wf_pingpong", &Tuning::wf_pingpong, 0, 3},
-        {"wf_stagger", &Tuning::wf_stagger, 0, 1},
         {"wf_walk", &Tuning::wf_walk, 0, 8},
         {"bvh_leaf", &Tuning::bvh_leaf, 1, 16},
     };
@@ -308,11 +301,6 @@ static int64_t *tuning_field(Tuning *t, const char *name, int64_t *lo, int64_t *
         *lo = 0;
         *hi = (int64_t)1 << 28;
         return &t->wf_paths;
-    }
-    if (!strcmp(name, "wf_tail_paths")) {
-        *lo = 0;
-        *hi = (int64_t)1 << 28;
-        return &t->wf_tail_paths;
     }
     for (const F &f : fs)
         if (!strcmp(name, f.n)) {
@@ -387,7 +375,7 @@ hipError_t launch_render(const DeviceScene &s, const FrameParams &P, double *out
         // Heart-only (or no marched shape): the single-function build
         // megakernel register budget (Tuning::mega_waves); depths > 8 use the
         // 2-wave build: their attenuation stacks are wider
-        switch (ws ? ws->tune.mega_waves : PT_DEFAULT_WAVES) {
+        switch (ws ? ws->tune.mega_waves : DEFAULT_WAVES) {
         case 2: render_tiles<4, 2, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         case 3: render_tiles<4, 3, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;
         case 5: render_tiles<4, 5, march::F_HEART><<<P.tile_count, 256, 0, st>>>(dscene(s), P, out); break;

@@ -30,7 +30,9 @@ struct DeviceScene {
 // reused by every frame of a renderer.
 // Per-kernel launch timing (pt_kernel_timing): HIP events recorded on the
 // launch stream around every render-path kernel while enabled.
-enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_TAIL = 5, K_WALK = 6, K_KINDS = 7 };
+// (kind 5 was the wavefront tail kernel, removed in round 6: its slot stays, always 0, so the ABI's array keeps
+// its layout)
+enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_RETIRED5 = 5, K_WALK = 6, K_KINDS = 7 };
 struct KernelTimer;
 KernelTimer *timer_new();
 void timer_free(KernelTimer *t);
@@ -54,13 +56,8 @@ struct Tuning {
     int wf_min_chunks = 1;           // at least this many sample chunks per frame (1..4096)
     int wf_bounce_waves = 3;         // wf_bounce register budget (2, 3, 4, 5, 6, 8)
     int wf_march_slice = 256;        // march-queue run dealt to a block (0 = contiguous share)
-    int wf_march_blocks_per_cu = 0;  // persistent march grid (0 = occupancy maximum)
-    int wf_side_priority = 0;        // the library's chunk streams' priority (-1 low, 0 normal, 1 high)
-    int wf_pingpong = 0;             // bit 0 bounce, bit 1 march launches of the chunk streams one at a time, in turn
-    int wf_stagger = 0;              // 1: chunk streams offset by 1/slots of a chunk (staggered sample chunks; C2 -1.2 %, depth 50 -3 %)
     int wf_walk = 5;                 // large-tree scenes without marched shapes: the BVH walk in its own kernel (wf_walk)
                                      // at this register budget, waves per SIMD (4, 5, 6, 8; 0: the walk in the bounce)
-    int64_t wf_tail_paths = 0;       // a chunk's live paths from which wf_tail runs them to their ends (0 = never)
     int bvh_leaf = 1;                // shapes per BVH leaf (1..16; C5 677 / 609 / 534 M samples/s at 1 / 2 / 4)
 };
 Tuning tuning_defaults();  // the measured defaults; a renderer changes them only through pt_renderer_set_option
@@ -87,7 +84,6 @@ struct WaveWorkspace {
     static constexpr int MAX_SLOTS = 4;
     hipStream_t side[MAX_SLOTS - 1] = {};
     hipEvent_t fork = nullptr, join[MAX_SLOTS - 1] = {}, reduced = nullptr;
-    hipEvent_t bev = nullptr, mev = nullptr;  // the last bounce / march launch of the cross-stream chains (Tuning::wf_pingpong)
     // recorded on the launch stream after a frame's last use of the workspace;
     // the next frame (on any stream) waits for it
     hipEvent_t done = nullptr;
@@ -99,7 +95,6 @@ struct WaveWorkspace {
     hipEvent_t args_ev = nullptr;
     bool args_pending = false;
     int device = -1;
-    int side_priority = 0;  // the priority the side streams were created with (Tuning::wf_side_priority)
 };
 void wave_workspace_free(WaveWorkspace *ws);
 

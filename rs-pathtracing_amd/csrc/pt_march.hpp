@@ -220,58 +220,23 @@ PT_HD double lin_room(double x, double c, Lin *L, double need = BIGD) {
     return ok ? room : 0.0;
 }
 
-// The exact per-step displacement of the literal adds fl(v + c) while v stays in its binade: R u, u = v's grid
-// 2^(e-52), R = rint(c / u) (lin_room's closed form: a round-half-even tie is the even neighbour only from an even
-// grid index).  *ok is false (and c comes back) where that closed form does not apply.
-PT_HD double grid_step(double v, double c, bool *ok) {
-    const double av = fabs(v);
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int e = __builtin_amdgcn_frexp_exp(v) - 1;
-#else
-    const int e = ilogb(av > 0.0 && av < 1e300 ? v : 1.0);
-#endif
-    const double q = ldexp(c, 52 - e), R = rint(q);
-    const bool tie = fabs(q - R) == 0.5, xodd = (f64_to_bits(v) & 1u) != 0;
-    *ok = av > 1e-280 && av < 1e300 && fabs(q) < 4.0e15 && !(tie && xodd);
-    return *ok ? ldexp(R, e - 52) : c;
-}
-// True if the B literal adds fl(v_j + c), v_0 = v, are all exactly v_j + cp, cp = grid_step(v, c) (ok: its
-// closed form applies; acp = |cp|): the points v + j cp, j <= B, and the adds' exact sums stay inside v's binade
-// by more than a grid step (conservative: the bound has relative slack for its own rounding; false is always
-// safe).  up: |v| grows (c has v's sign).
-PT_HD bool stays_in_binade(double v, bool up, double acp, double B) {
-    const double av = fabs(v);
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int e = __builtin_amdgcn_frexp_exp(v) - 1;
-#else
-    const int e = ilogb(av > 0.0 && av < 1e300 ? v : 1.0);
-#endif
-    const double u = ldexp(1.0, e - 52), lo = ldexp(1.0, e);
-    const double reach = ((B + 1.0) * acp + 4.0 * u) * (1.0 + 0x1p-48);  // >= B |cp| + |c| + 2u
-    return up ? av + reach < 2.0 * lo - 2.0 * u : av - reach >= lo + 2.0 * u;
-}
-
 // x after n literal additions fl(x + c), exactly, across any number of binade
 // edges: closed form inside each binade, literal adds in the thin zone at an
-// edge and within PT_ADV_NZ |c| of zero (a coordinate crossing zero passes
+// edge and within ADV_NZ |c| of zero (a coordinate crossing zero passes
 // ~2 log2(|x| / |c|) binades; the ones near zero hold a few steps each, and a
 // closed-form segment costs ~150 instructions against ~5 per literal add: C2
 // one-stream march 183 -> 172 ms).  Each coordinate's sequence is independent of the
 // others, so p, t can be advanced separately.
-#ifndef PT_ADV_NZB
-#define PT_ADV_NZB 4  // literal adds per trip in the near-zero zone
-#endif
-#ifndef PT_ADV_NZ
-#define PT_ADV_NZ 24.0  // |x| below this many |c|: literal adds (the binades there hold a few steps each; 0: off)
-#endif
+constexpr int ADV_NZB = 4;         // literal adds per trip in the near-zero zone
+constexpr double ADV_NZ = 24.0;    // |x| below this many |c|: literal adds (the binades there hold a few steps each)
 PT_HD double advance(double x, double c, double n) {
     PT_MHOOK(adv_begin);
     while (n > 0.0) {
-        if (PT_ADV_NZ > 0.0 && fabs(x) < PT_ADV_NZ * fabs(c)) {
-            // near zero every binade holds only a few steps: PT_ADV_NZB
+        if (fabs(x) < ADV_NZ * fabs(c)) {
+            // near zero every binade holds only a few steps: ADV_NZB
             // literal adds per trip instead of one closed-form segment per binade
 #pragma unroll
-            for (int j = 0; j < PT_ADV_NZB; j++) {
+            for (int j = 0; j < ADV_NZB; j++) {
                 PT_MPROF(lit_adds);
                 const bool go = n > 0.0;
                 x = go ? x + c : x;
@@ -299,7 +264,7 @@ PT_HD double advance(double x, double c, double n) {
 // One segment of advance(): the closed form to the end of x's binade segment
 // (and the literal add leaving it), or one literal add in an edge zone.
 PT_HD void seg_step(double &x, double c, double &n) {
-    if (PT_ADV_NZ > 0.0 && fabs(x) < PT_ADV_NZ * fabs(c)) {  // near zero: a literal add (see advance)
+    if (fabs(x) < ADV_NZ * fabs(c)) {  // near zero: a literal add (see advance)
         x = x + c;
         n -= 1.0;
         return;
@@ -382,10 +347,6 @@ PT_HD int64_t steps_in_range(double t, double s, double start, double end, int64
 struct Poly {
     double g[7];                       // coefficients of g(j)
     double ax, ay, az, cx, cy, cz;     // |p0|, |ch| for the magnitude bound
-    // drift weights: 0 for a coordinate whose step points are exactly p0 + j ch over the block (it stays in its
-    // binade, ch its exact grid step: stays_in_binade), 1 for one that may cross a binade edge (its points then
-    // drift from the line by the adds' rounding, which the margin covers)
-    double wx = 1.0, wy = 1.0, wz = 1.0;
 };
 
 // The Heart's expansion, by coefficient (fewer live temporaries than the
@@ -468,7 +429,7 @@ PT_HD double heart_margin(const Poly &P, double b) {
     double gx = 6.0 * xm * am2 + 2.0 * xm * z3;
     double gy = 13.5 * ym * am2 + 0.225 * ym * z3;
     double gz = 6.0 * zm * am2 + 3.0 * x2 * z2 + 0.3375 * y2 * z2;
-    double drift = b * 2.3e-16 * (P.wx * gx * xm + P.wy * gy * ym + P.wz * gz * zm);  // ulp(v)/2 <= 2^-53 |v| (2.3e-16 > 2^-52)
+    double drift = b * 2.3e-16 * (gx * xm + gy * ym + gz * zm);  // ulp(v)/2 <= 2^-53 |v| (2.3e-16 > 2^-52)
     return 1e-15 + e256 * mag + drift;
 }
 
@@ -482,7 +443,7 @@ PT_HD double poly_margin(const FParams &F, const Poly &P, double b) {
     // p_j = p0 + j*c + delta_j with |delta_j,k| <= j*ulp_k/2 (each literal
     // add rounds once): add max|grad f| . |delta| over the block.
     const DM m = shape_mag_k<FK>(F, xm, ym, zm);
-    const double drift = b * 2.3e-16 * (P.wx * m.gx * xm + P.wy * m.gy * ym + P.wz * m.gz * zm);  // ulp(v)/2 <= 2^-53 |v|
+    const double drift = b * 2.3e-16 * (m.gx * xm + m.gy * ym + m.gz * zm);  // ulp(v)/2 <= 2^-53 |v|
     return 1e-15 + e256 * m.v + drift;
 }
 
@@ -513,14 +474,9 @@ PT_HD bool poly_sign_definite(const FParams &F, const Poly &P, double b, double 
 }
 
 constexpr int FOLD_MAX = 3;     // literal steps an iteration may take when the predicted crossing is that close
-#ifndef PT_LIT_DOUBLE
-#define PT_LIT_DOUBLE 1  // literal batches after failed proofs double per failure in a row (0: one step each)
-#endif
-#ifndef PT_MARCH_GRID
-#define PT_MARCH_GRID 0  // proofs along the coordinates' exact grid steps, no drift term for in-binade blocks
-#endif
-constexpr int LIT_BATCH = PT_LIT_DOUBLE ? 2 : 1;  // literal steps after a proof that proved no block
-constexpr int LIT_DOUBLINGS = PT_LIT_DOUBLE ? 5 : 0;
+// literal batches after failed proofs double per failure in a row (round 5; one step each: C2 1978 vs 2068)
+constexpr int LIT_BATCH = 2;  // literal steps after a proof that proved no block
+constexpr int LIT_DOUBLINGS = 5;
 constexpr int MAX_LEVELS = 40;  // de Casteljau halvings per prefix search (capping them: more iterations, slower)
 // Longest provable prefix of a block: the largest integer b <= B such that
 // sgn * (f64 heart_f at p_j) > 1e-15 for every j in [1, b] (so neither the
@@ -672,10 +628,7 @@ struct MarchState {
 // M_GUARD: the march was dropped by MARCH_GUARD (callers take it as a miss
 // and count it: pt_march_guard_drops).
 enum MarchStatus : int { M_RUNNING = 0, M_DONE = 1, M_MISS = 2, M_GUARD = 3 };
-#ifndef PT_MARCH_GUARD
-#define PT_MARCH_GUARD (1u << 24)
-#endif
-constexpr uint32_t MARCH_GUARD = PT_MARCH_GUARD;  // (lowered only in timing experiments)
+constexpr uint32_t MARCH_GUARD = 1u << 24;
 
 // Start of the march on a bound interval [start, end] already known
 // (intersect_bound, ray_marching.rs:27-31), object-space ray (o, d).
@@ -759,18 +712,10 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
         if (bmax >= 2.0) {
             Poly P;
             PT_MREG(poly_begin);
-            // the polynomial along the coordinates' exact grid steps (no drift while they stay in their binades)
-            {
-                bool okx, oky, okz;
-                okx = oky = okz = false;
-                const double ex = PT_MARCH_GRID ? grid_step(m.px, cx, &okx) : cx,
-                             ey = PT_MARCH_GRID ? grid_step(m.py, cy, &oky) : cy,
-                             ez = PT_MARCH_GRID ? grid_step(m.pz, cz, &okz) : cz;
-                func_poly<FK>(m.F, m.px, m.py, m.pz, ex, ey, ez, &P);
-                P.wx = okx ? 0.0 : 1.0;  // (final once the block is sized: stays_in_binade)
-                P.wy = oky ? 0.0 : 1.0;
-                P.wz = okz ? 0.0 : 1.0;
-            }
+            // the polynomial along the steps, every coordinate with its drift term (proofs along the exact grid
+            // steps of in-binade coordinates, without the drift, took fewer iterations but spilled the march
+            // kernel: C2 2041 vs 2068, round 5, removed in round 6)
+            func_poly<FK>(m.F, m.px, m.py, m.pz, cx, cy, cz, &P);
             if (STATS) st->tries++;
             // longest provable prefix of a block sized from the predicted
             // crossing (the margin scales with the block, so a block far
@@ -794,9 +739,6 @@ PT_HD int march_iter(MarchState &m, MarchStats *st) {
             if (!em) B = B > bmax ? bmax : (B < 2.0 ? 2.0 : B);
             // the step just before the predicted crossing
             const double target = em ? 0.0 : ceil(guess) - 1.0;
-            P.wx = P.wx == 0.0 && stays_in_binade(m.px, (m.px >= 0.0) == (cx >= 0.0), P.cx, B) ? 0.0 : 1.0;
-            P.wy = P.wy == 0.0 && stays_in_binade(m.py, (m.py >= 0.0) == (cy >= 0.0), P.cy, B) ? 0.0 : 1.0;
-            P.wz = P.wz == 0.0 && stays_in_binade(m.pz, (m.pz >= 0.0) == (cz >= 0.0), P.cz, B) ? 0.0 : 1.0;
             PT_MREG(prefix_begin);
             double good = poly_prefix<FK>(m.F, P, B, sgn, target, em ? EM_LEVELS : MAX_LEVELS);
             PT_MREG(prefix_end);

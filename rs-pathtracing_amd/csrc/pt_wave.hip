@@ -63,10 +63,8 @@ using dev::V3;
 // field sits at an immediate offset from one per-lane address: with one array
 // per field the loop-invariant field bases of the two sets were 22 SGPR pairs,
 // and the bounce kernel spilled 65 SGPRs to VGPR lanes (round 5).
-#ifndef PT_PACK_META
-#define PT_PACK_META 1  // who and the attenuation-stack count in one word, the depth from the iteration (72 B state)
-#endif
-// PT_PACK_META: a live path's depth at bounce `it` is depth - (it - 1) for every path (each bounce before it
+// Who and the attenuation-stack count share one word, and the depth comes from the iteration (72 B of state per
+// path; round 5): a live path's depth at bounce `it` is depth - (it - 1) for every path (each bounce before it
 // shaded it once and scattered), so only the stack count is state; it shares a word with the pending hit's
 // shape: (who + 1) | count << 25 (shapes < 2^24: the BVH's leaf index bound; count <= depth <= 64).
 constexpr uint32_t WHO_MASK = (1u << 25) - 1u;
@@ -78,10 +76,10 @@ __host__ __device__ __forceinline__ int unpack_who(uint32_t w) { return (int)(w 
 struct PathSoA {
     char *base;
     size_t cap;  // a multiple of 64
-    static constexpr size_t BYTES = 8 * 8 + (PT_PACK_META ? 2 : 3) * 4;  // per path
+    static constexpr size_t BYTES = 8 * 8 + 2 * 4;  // per path
     static constexpr uint32_t BLK = 64, BLK_BYTES = (uint32_t)BYTES * BLK;
     enum F8 : int { OX, OY, OZ, DX, DY, DZ, T, RNG };
-    enum F4 : int { WHO, SID, META };  // (META: without PT_PACK_META only)
+    enum F4 : int { WHO, SID };
     // the 8-byte fields of position k: d8(k)[f * 64]; the 4-byte ones: d4(k)[f * 64]
     __host__ __device__ double *d8(uint32_t k) const {
         return (double *)(base + (size_t)(k / BLK) * BLK_BYTES) + (k % BLK);
@@ -90,7 +88,7 @@ struct PathSoA {
         return (uint32_t *)(base + (size_t)(k / BLK) * BLK_BYTES + 8 * 8 * BLK) + (k % BLK);
     }
     __host__ __device__ double &t(uint32_t k) const { return d8(k)[T * BLK]; }  // best hit t
-    // the word holding the best hit's shape (-1: miss; PT_PACK_META: packed with the stack count, pack_who)
+    // the word holding the best hit's shape (-1: miss), packed with the stack count (pack_who)
     __host__ __device__ uint32_t &who(uint32_t k) const { return d4(k)[WHO * BLK]; }
 };
 
@@ -233,9 +231,9 @@ template <typename T>
 __device__ __forceinline__ T ld_path(const T *p) {
     return *p;
 }
-// depth, count: the path's depth and attenuation-stack count (PT_PACK_META stores only the count, with who)
+// count: the path's attenuation-stack count (stored with who; the depth follows from the iteration)
 __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_t id, const Ray &ray, double best,
-                                           int who, uint64_t rng, uint32_t depth, uint32_t count) {
+                                           int who, uint64_t rng, uint32_t count) {
     double *a = S.d8(k);
     uint32_t *b = S.d4(k);
     constexpr uint32_t B = PathSoA::BLK;
@@ -246,13 +244,12 @@ __device__ __forceinline__ void store_path(const PathSoA &S, uint32_t k, uint32_
     st_path(a + PathSoA::DY * B, ray.d.y);
     st_path(a + PathSoA::DZ * B, ray.d.z);
     st_path(a + PathSoA::T * B, best);
-    st_path(b + PathSoA::WHO * B, PT_PACK_META ? pack_who(who, count) : (uint32_t)who);
+    st_path(b + PathSoA::WHO * B, pack_who(who, count));
     st_path((uint64_t *)a + PathSoA::RNG * B, (uint64_t)rng);
-    if (!PT_PACK_META) st_path(b + PathSoA::META * B, depth | count << 8);
     st_path(b + PathSoA::SID * B, id);
 }
 // The state of position p: slot id, ray, rng, pending hit (who, t), attenuation-stack count, and the depth
-// (PT_PACK_META: depth_it, the depth of every path at this bounce).
+// (depth_it: the depth of every path at this bounce).
 __device__ __forceinline__ void load_path(const PathSoA &S, uint32_t p, uint32_t *id, Ray *ray, uint64_t *rng,
                                           uint32_t depth_it, uint32_t *depth, uint32_t *count, int *who,
                                           double *best) {
@@ -264,16 +261,9 @@ __device__ __forceinline__ void load_path(const PathSoA &S, uint32_t p, uint32_t
     ray->d = dev::v3(ld_path(a + PathSoA::DX * B), ld_path(a + PathSoA::DY * B), ld_path(a + PathSoA::DZ * B));
     *rng = ld_path((const uint64_t *)a + PathSoA::RNG * B);
     const uint32_t w = ld_path(b + PathSoA::WHO * B);
-    if (PT_PACK_META) {
-        *who = unpack_who(w);
-        *count = w >> 25;
-        *depth = depth_it;
-    } else {
-        const uint32_t meta = ld_path(b + PathSoA::META * B);
-        *who = (int)w;
-        *count = meta >> 8;
-        *depth = meta & 0xffu;
-    }
+    *who = unpack_who(w);
+    *count = w >> 25;
+    *depth = depth_it;
     *best = ld_path(a + PathSoA::T * B);
 }
 
@@ -295,32 +285,7 @@ __device__ __forceinline__ void slot_pixel(const FrameParams &P, const WfView &v
 
 // points along a march job's chord whose sign of f predicts a hit (queue
 // order only; 0: march -25 %, profiles/r3/ab_round3_experiments.txt)
-#ifndef PT_WF_PREDICT
-#define PT_WF_PREDICT 4
-#endif
-constexpr int WF_PREDICT = PT_WF_PREDICT;
-
-#ifndef PT_WALK_ULIST_IN_BOUNCE
-#define PT_WALK_ULIST_IN_BOUNCE 0  // the split bounce traces the uniform list, wf_walk only the BVH
-#endif
-#ifndef PT_WALK_XCD
-#define PT_WALK_XCD 0  // XCD-aware block order in the walk kernel
-#endif
-#ifndef PT_MARCH_SPREAD
-#define PT_MARCH_SPREAD 1  // a short march queue dealt in runs of count / blocks (1), or always in slice runs (0)
-#endif
-
-#ifndef PT_MARCH_WAVE_RUNS
-#define PT_MARCH_WAVE_RUNS 1  // a march queue shorter than the grid's lanes dealt one run per wave (1), or per block (0)
-#endif
-
-#ifndef PT_WAVE_COMPACT
-#define PT_WAVE_COMPACT 1  // bounce outputs compacted per wave (survivors first): 1 on, 0 every input position stored
-#endif
-
-#ifndef PT_WF_BOUNCE_WAVES
-#define PT_WF_BOUNCE_WAVES 3  // default waves per SIMD the register budget must allow
-#endif
+constexpr int WF_PREDICT = 4;
 
 // One bounce for every live path of iteration `it` (it == 0: camera rays).
 // DIAG: wave-level s_memtime cycles per section, each section ended by a
@@ -328,8 +293,8 @@ constexpr int WF_PREDICT = PT_WF_PREDICT;
 // only): list load, state loads, shade, unwind, trace, march pre-check,
 // stores; summed into diag[36..42].
 // SPLIT (the large-tree builds without marched shapes, C5): the kernel only shades and stores the new ray; wf_walk
-// traces it after the compaction (PT_WF_WALK).
-template <int NW, bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false, bool BIGBVH = false, bool SPLIT = false>
+// traces it after the compaction (Tuning::wf_walk).
+template <bool FIRST, int WAVES, int FK = march::F_ANY, bool EXT = false, bool BIGBVH = false, bool SPLIT = false>
 __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict__ A, int it,
                                                         unsigned long long *diag = nullptr) {
     // input: the id-sorted list of live paths (iteration 0: every slot)
@@ -417,14 +382,9 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
                 }
             }
         }
-        if (live && SPLIT) {  // the ray is traced by wf_walk (PT_WALK_ULIST_IN_BOUNCE: the uniform list here)
+        if (live && SPLIT) {  // the ray is traced by wf_walk
             best = __builtin_inf();
             who = -1;
-            if (PT_WALK_ULIST_IN_BOUNCE) {
-                const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-                dev::closest_nomarch<false, false, true, false, 1>(kargs(A).sc, ray, inv, T_MIN, &best, &who, nullptr,
-                                                                   depth == 0);
-            }
         } else if (live) {
             PT_LP(TRACE);
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
@@ -459,7 +419,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
                 live = false;
             }
         }
-#if PT_WAVE_COMPACT
         // The wave's surviving paths (live, or waiting for a march) go to consecutive output positions from the
         // wave's first one, in input (= id) order, and the positions after them get status 0: the ended paths'
         // state is not written, and the next bounce gathers from runs with holes only at wave ends (round 5).
@@ -467,9 +426,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
         const uint64_t keep = __ballot(live);
         const uint32_t k = wbase + (uint32_t)__popcll(keep & ((1ull << (threadIdx.x & 63)) - 1ull));
         if (i < count && (threadIdx.x & 63) >= (uint32_t)__popcll(keep)) v.status[i] = 0u;
-#else
-        const uint32_t k = i;  // every input position's state is written (ended paths too: whole lines; storeab)
-#endif
         if (need_march && v.jo) {  // the march kernel starts from here (one marched shape)
             PT_LP(PRE_JOB);
             // the 64 B record in four 16-byte non-temporal stores (as eight 8-byte ones: the
@@ -498,8 +454,8 @@ __global__ __launch_bounds__(256, WAVES) void wf_bounce(const WfArgs *__restrict
             }
         }
         if (i < count) PT_LP(STORE);
-        if (i < count && (!PT_WAVE_COMPACT || live)) {
-            store_path(v.out, k, id, ray, best, who, rng.s, depth, (uint32_t)stk.n);
+        if (i < count && live) {
+            store_path(v.out, k, id, ray, best, who, rng.s, (uint32_t)stk.n);
             v.status[k] = live ? (need_march ? (long_job ? 7u : 3u) : 1u) : 0u;
         }
         PT_BSTAMP(6)
@@ -596,10 +552,7 @@ struct CpLayout {
 // on the device) with at most CP_GRID blocks, each looping over tiles: a late
 // iteration's few live paths no longer launch a grid of the chunk's size
 // (three launches of ~11k blocks cost ~40 us even with nothing to do, round 5).
-#ifndef PT_CP_GRID
-#define PT_CP_GRID 2048  // (0: one block per tile of the chunk, as before round 5)
-#endif
-constexpr uint32_t CP_GRID = PT_CP_GRID;
+constexpr uint32_t CP_GRID = 2048;
 __device__ __forceinline__ uint32_t cp_n(const uint32_t *n_dev, uint32_t n_host) { return n_dev ? *n_dev : n_host; }
 
 // per tile: (live, long march, short march) counts
@@ -749,22 +702,22 @@ __global__ __launch_bounds__(256) void cp_scatter(const uint8_t *__restrict__ st
 // Measured and dropped (profiles/r2/ab_round2_experiments.txt): a per-wave phase vote,
 // batched job switches, several march units per trip, non-temporal result stores.
 constexpr uint32_t WF_BOUNCE_CAP = 8192;  // bounce grid (blocks) after the first iteration; threads loop over the live list
-#ifndef PT_WF_MARCH_WAVES
-#define PT_WF_MARCH_WAVES 4  // waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs, 20 B: 1273; 3: 1261)
-#endif
+// waves per SIMD the march kernel's registers must allow (C2: 5 waves spill 100 B/lane: 1187; 4: 128 VGPRs,
+// 20 B: 1273; 3: 1261 M samples/s, round 1)
+constexpr int WF_MARCH_WAVES = 4;
 struct MarchJob {
     uint32_t id;
     Ray ray;
     double best;
     int who;
-    uint32_t hi;  // PT_PACK_META: the stack-count bits of the who word, written back unchanged
+    uint32_t hi;  // the stack-count bits of the who word, written back unchanged
 };
 __device__ __forceinline__ void job_who(MarchJob *j, uint32_t w) {
-    j->who = PT_PACK_META ? unpack_who(w) : (int)w;
-    j->hi = PT_PACK_META ? (w & ~WHO_MASK) : 0u;
+    j->who = unpack_who(w);
+    j->hi = w & ~WHO_MASK;
 }
 __device__ __forceinline__ uint32_t job_who_word(int who, uint32_t hi) {
-    return PT_PACK_META ? (uint32_t)(who + 1) | hi : (uint32_t)who;
+    return (uint32_t)(who + 1) | hi;
 }
 
 __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob *j) {
@@ -781,7 +734,7 @@ __device__ __forceinline__ void load_job(const PathSoA &S, uint32_t p, MarchJob 
 // 0 cheap, 1 select, 2 advance, 3 proof), lanes per kind and the trip's
 // s_memtime cycles, summed per wave into diag[0..35] (tuning only).
 template <int FK = march::F_ANY>
-__global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs *__restrict__ A, int it,
+__global__ __launch_bounds__(256, WF_MARCH_WAVES) void wf_march(const WfArgs *__restrict__ A, int it,
                                                                    unsigned long long *diag, uint32_t slice_max) {
     __shared__ uint32_t head;
     const bool DIAG = PT_WAVE_DIAG && diag;  // (a diagnostics build with pt_wave_diag enabled)
@@ -799,7 +752,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
     // one block's waves: each wave's trips then cost only its own jobs' code
     // (a persistent launch lasts as long as its slowest wave; round 5).
     const uint32_t slice = slice_max == 0 ? 0u
-                           : (PT_MARCH_SPREAD && count / gridDim.x < slice_max ? max(1u, count / gridDim.x) : slice_max);
+                           : (count / gridDim.x < slice_max ? max(1u, count / gridDim.x) : slice_max);
     uint32_t per, lo;
     if (slice == 0) {
         per = (count + gridDim.x - 1) / gridDim.x;
@@ -826,7 +779,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
     // lasts as long as its slowest wave: dealt per block, a late queue of ~10
     // jobs per block put them all in the block's first wave (round 5).
     const uint32_t nwv = blockDim.x >> 6;
-    const bool runs_w = PT_MARCH_WAVE_RUNS && slice_max != 0 && count < G * blockDim.x;
+    const bool runs_w = slice_max != 0 && count < G * blockDim.x;
     const uint32_t kw = runs_w ? (count + G * nwv - 1) / (G * nwv) : 0u;
     const uint32_t pw = ((threadIdx.x >> 6) * G + blockIdx.x) * kw + (threadIdx.x & 63);
     uint32_t q = threadIdx.x;
@@ -972,7 +925,7 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 }
 
 // The BVH walk of the large-tree scenes without marched shapes (C5) as its own
-// kernel (PT_WF_WALK, round 5): the walk is latency-bound (a chain of
+// kernel (Tuning::wf_walk, round 5): the walk is latency-bound (a chain of
 // dependent node loads per lane, ~70 % of the bounce's wave cycles waiting on
 // memory), and inside the bounce kernel its lanes run at the bounce's register
 // budget (118 VGPRs: 4 waves per SIMD).  Alone it needs far fewer registers,
@@ -981,47 +934,34 @@ __global__ __launch_bounds__(256, PT_WF_MARCH_WAVES) void wf_march(const WfArgs 
 // the ray each bounce stored, traced through the uniform list and the BVH
 // (closest_nomarch, the same code and tie rule as the bounce's trace), and
 // (best, who) written back in place; the next bounce shades them.
-#ifndef PT_WALK_QN
-#define PT_WALK_QN 1  // the walk reads the quantized 16-byte nodes (DNodeQ) when the scene has them (0: DNodeC)
-#endif
-#ifndef PT_WALK_OCT
-#define PT_WALK_OCT 1  // a block's 256 rays regrouped by direction octant before the walk (0: in list order;
-                       // 2: by octant and major axis)
-#endif
+// QN: the walk reads the quantized 16-byte nodes (DNodeQ; a tree without them takes the 32-byte DNodeC).
 template <int WAVES, bool QN>
 __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__ A, int it) {
     __shared__ uint32_t pos[256];      // the block's list positions, grouped by octant
-    constexpr uint32_t NB = PT_WALK_OCT == 2 ? 25u : 9u;  // groups (the last: no ray)
+    constexpr uint32_t NB = 9u;  // groups: the 8 octants, and the last for no ray
     __shared__ uint32_t wcount[4][NB];  // rays per (wave, group)
     const uint32_t count = kargs(A).v.cnt[(it + 1) * 4 + 0];
     const uint32_t stride = gridDim.x * blockDim.x;
     // the trace after bounce it is shaded at depth P.depth - it: at 0 only hit or miss matters
     const bool any = kargs(A).P.depth == (uint32_t)it;
-    // PT_WALK_XCD: the workgroups are dealt to the 8 XCDs round-robin by id, so block b takes the rays of logical
-    // block (b mod 8) * (blocks / 8) + b / 8: each XCD walks a contiguous (pixel-coherent) eighth of every
-    // grid-wide round, and its own L2 holds that region's nodes
-    const uint32_t lb = PT_WALK_XCD && gridDim.x % 8u == 0 ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u
-                                                          : blockIdx.x;
-    for (uint32_t base = lb * blockDim.x; base < count; base += stride) {  // (block-uniform)
+    // (an XCD-aware block order, each XCD walking a contiguous eighth of every grid-wide round, measured slower:
+    // round 5)
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += stride) {  // (block-uniform)
         const WfArgs &a = kargs(A);
         const WfView &v = a.v;
         const uint32_t i = base + threadIdx.x;
         constexpr uint32_t B = PathSoA::BLK;
         uint32_t p;
-        if (PT_WALK_OCT) {
+        {
             // Counting sort of the block's rays by the octant of their direction (the BVH layout they walk),
             // stable, so each group keeps the list's pixel order: a wave then walks one or two layouts with
             // neighbouring origins instead of up to eight (the rays after a diffuse bounce spread over the
-            // hemisphere's octants).
+            // hemisphere's octants; octant and major axis, 24 groups, scattered the pixel order: slower, r5s).
             const uint32_t q = i < count ? v.list[i] : 0u;
             const double *d = v.out.d8(q);
             const double dx = d[PathSoA::DX * B], dy = d[PathSoA::DY * B], dz = d[PathSoA::DZ * B];
             uint32_t oct = (__builtin_signbit(dx) ? 1u : 0u) | (__builtin_signbit(dy) ? 2u : 0u) |
                            (__builtin_signbit(dz) ? 4u : 0u);
-            if (PT_WALK_OCT == 2) {  // and the direction's major axis
-                const double ax = fabs(dx), ay = fabs(dy), az = fabs(dz);
-                oct = oct * 3u + (ax >= ay && ax >= az ? 0u : (ay >= az ? 1u : 2u));
-            }
             if (i >= count) oct = NB - 1u;
             const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
             uint32_t rank = 0;
@@ -1038,8 +978,6 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
             __syncthreads();
             p = pos[threadIdx.x];
             __syncthreads();  // (pos and wcount are rewritten by the next trip)
-        } else {
-            p = i < count ? v.list[i] : 0u;
         }
         if (i < count) {  // (the block's first count - base positions hold its rays)
             const double *d = v.out.d8(p);
@@ -1049,133 +987,11 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
             const V3 inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
             double best = __builtin_inf();
             int who = -1;
-            if (PT_WALK_ULIST_IN_BOUNCE) {  // the bounce's uniform-list hit
-                best = d[PathSoA::T * B];
-                who = unpack_who(v.out.who(p));
-            }
-            dev::closest_nomarch<false, false, true, QN, PT_WALK_ULIST_IN_BOUNCE ? 2 : 3>(a.sc, ray, inv, T_MIN, &best,
-                                                                                          &who, nullptr, any);
+            dev::closest_nomarch<false, false, true, QN>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
             v.out.t(p) = best;
             uint32_t &w = v.out.who(p);
-            w = PT_PACK_META ? (w & ~WHO_MASK) | (uint32_t)(who + 1) : (uint32_t)who;
+            w = (w & ~WHO_MASK) | (uint32_t)(who + 1);
         }
-    }
-}
-
-// The tail of a chunk (round 5).  The live paths of a chunk decay by ~10 %
-// per bounce; once few are left, each iteration's launches are latency-bound:
-// a persistent march launch lasts as long as its slowest job (~200-250 us at
-// depth 50, whatever the queue length), a bounce and its compaction ~60 us,
-// and a depth-50 chunk spent a quarter of its time in 30 such iterations
-// (profiles/r5/kt_iters_c2_depth50_final.txt).  wf_tail runs before the
-// bounce of iteration it: when that bounce's live list holds at most
-// max_paths paths, its persistent lanes take the paths one at a time and run
-// each to its end -- shade the pending hit, trace, select and march, shade
-// again, ... (trace_pixel's phase machine, dev::shade, the same march code as
-// wf_march's selecting path) -- storing the leaf record the reduce unwinds.  A
-// path's operations and values are the ones the per-iteration kernels would
-// have produced.  The last block to finish sets the live count of iteration
-// `it` to 0, so the chunk's remaining launches find no work.  cnt[it * 4 + 3]
-// (it >= 1: unused) is the path counter, cnt[it * 4 + 2] (rewritten by this
-// iteration's compaction) the finished-block counter.
-enum TailPhase : int { TP_TRACE = 0, TP_SELECT = 1, TP_MARCH = 2, TP_SHADE = 3 };
-#ifndef PT_WF_TAIL_WAVES
-#define PT_WF_TAIL_WAVES 2  // waves per SIMD the tail kernel's registers must allow
-#endif
-template <int FK, bool EXT, bool BIGBVH>
-__global__ __launch_bounds__(256, PT_WF_TAIL_WAVES) void wf_tail(const WfArgs *__restrict__ A, int it,
-                                                                 uint32_t max_paths) {
-    const uint32_t count = kargs(A).v.cnt[it * 4 + 0];
-    if (count == 0 || count > max_paths) return;  // (every block sees the same count)
-    {
-        const uint32_t depth_it = kargs(A).P.depth + 1u - (uint32_t)it;
-        bool have = false;
-        uint32_t id = 0, depth = 0;
-        int phase = TP_SHADE, who = -1, km = 0, mshape = -1;
-        double best = 0.0;
-        Ray ray;
-        V3 inv = dev::v3(0.0, 0.0, 0.0);
-        dev::Rng rng{0};
-        MemStack stk{nullptr, 0, 0, nullptr};
-        march::MarchState ms;
-        march::MarchStats mst{0, 0, 0, 0};
-        for (;;) {
-            const WfArgs &a = kargs(A);
-            const WfView &v = a.v;
-            if (!have) {
-                // the wave's lanes without a path take the next ones of the list (one atomic per wave)
-                const uint64_t need = __ballot(1);  // (the lanes still in the loop all need one here)
-                const int lead = __builtin_ctzll(need);
-                const uint32_t n = (uint32_t)__popcll(need);
-                uint32_t b = 0;
-                if ((int)lane_id() == lead) b = atomicAdd(&v.cnt[it * 4 + 3], n);
-                b = __shfl(b, lead, 64);
-                const uint32_t q = b + (uint32_t)__popcll(need & ((1ull << lane_id()) - 1ull));
-                if (q >= count) break;
-                uint32_t c;
-                load_path(v.in, v.list[q], &id, &ray, &rng.s, depth_it, &depth, &c, &who, &best);
-                stk = MemStack{v.ids + id, (size_t)v.cap, (int)c, EXT ? v.att + id : nullptr};
-                have = true;
-                phase = TP_SHADE;
-            }
-            if (phase == TP_TRACE) {
-                inv = dev::v3(1.0 / ray.d.x, 1.0 / ray.d.y, 1.0 / ray.d.z);
-                best = __builtin_inf();
-                who = -1;
-                // shaded at depth 0, only hit or miss matters (as the bounce kernel's `any`)
-                const bool any = depth == 0;
-                dev::closest_nomarch<false, EXT, BIGBVH>(a.sc, ray, inv, T_MIN, &best, &who, nullptr, any);
-                km = 0;
-                phase = (any && who >= 0) || FK == march::F_NONE ? TP_SHADE : TP_SELECT;
-            }
-            if constexpr (FK != march::F_NONE) {  // (a scene without marched shapes never selects)
-            if (phase == TP_MARCH) {
-                const int st = march::march_step<false, true, FK>(ms, &mst);
-                if (st != march::M_RUNNING) {
-                    if (st == march::M_GUARD) dev::note_guard(a.sc.guard);
-                    // final test of ray_marching.rs:55-57 against [T_MIN, best], then the tie rule
-                    if (st == march::M_DONE && !(ms.t < T_MIN || ms.t > best) && (ms.t < best || mshape > who)) {
-                        best = ms.t;
-                        who = mshape;
-                    }
-                    phase = TP_SELECT;
-                }
-            }
-            if (phase == TP_SELECT) {
-                // next marched shape whose bound is entered before `best`
-                const dev::Scene &sc = a.sc;
-                phase = TP_SHADE;
-                while (km < sc.nmarch) {
-                    const int sh = sc.march[km++];
-                    const DBox &bx = sc.boxes[sh];
-                    if (!dev::slab(bx.lo, bx.hi, ray, inv, T_MIN, best)) continue;
-                    const DShape &S = sc.shapes[sh];
-                    const V3 o = dev::xf_point(S.inv, ray.o), d = dev::xf_vector(S.inv, ray.d);
-                    if (march::march_begin<FK>(dev::shape_params(S), S.p[0], S.depth, o.x, o.y, o.z, d.x, d.y, d.z,
-                                               &ms)) {
-                        mshape = sh;
-                        phase = TP_MARCH;
-                        break;
-                    }
-                }
-            }
-            }
-            if (phase == TP_SHADE) {
-                V3 leaf;
-                if (dev::shade<false, FK, EXT>(a.sc, who, best, ray, depth, stk, rng, a.P.s11, &leaf)) {
-                    end_path(v, id, stk, leaf);
-                    have = false;
-                } else {
-                    phase = TP_TRACE;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        uint32_t *cnt = kargs(A).v.cnt;
-        if (atomicAdd(&cnt[it * 4 + 2], 1u) == gridDim.x - 1) cnt[it * 4 + 0] = 0u;  // every block has read it
     }
 }
 
@@ -1297,10 +1113,8 @@ void wave_workspace_free(WaveWorkspace *ws) {
     if (ws->fork) (void)hipEventDestroy(ws->fork);
     if (ws->reduced) (void)hipEventDestroy(ws->reduced);
     if (ws->done) (void)hipEventDestroy(ws->done);
-    if (ws->bev) (void)hipEventDestroy(ws->bev);
-    if (ws->mev) (void)hipEventDestroy(ws->mev);
     if (ws->args_ev) (void)hipEventDestroy(ws->args_ev);
-    ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = ws->args_ev = nullptr;
+    ws->fork = ws->reduced = ws->done = ws->args_ev = nullptr;
     ws->used = false;
     timer_free(ws->timer);
     ws->timer = nullptr;
@@ -1311,7 +1125,7 @@ void wave_workspace_free(WaveWorkspace *ws) {
     ws->bytes = 0;
 }
 
-// The launches' argument blocks: a pinned host staging buffer and its device copy (render_wave_nw).
+// The launches' argument blocks: a pinned host staging buffer and its device copy (render_wave).
 static void free_args(WaveWorkspace *ws) {
     if (ws->args_pending && ws->args_ev) (void)hipEventSynchronize(ws->args_ev);
     if (ws->args_host) (void)hipHostFree(ws->args_host);
@@ -1373,68 +1187,49 @@ static bool walk_split(const dev::Scene &sc, const Tuning &tu) {
     return tu.wf_walk && !sc.ext && sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0;
 }
 
-template <int NW, bool FIRST>
+template <bool FIRST>
 static void launch_bounce(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it,
                           unsigned long long *diag, int fkind, int waves, bool split) {
     if (split) {  // shade and store the new ray only: wf_walk traces it
         switch (waves) {
-        case 4: wf_bounce<NW, FIRST, 4, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
-        case 5: wf_bounce<NW, FIRST, 5, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
-        default: wf_bounce<NW, FIRST, 3, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 4: wf_bounce<FIRST, 4, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 5: wf_bounce<FIRST, 5, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
+        default: wf_bounce<FIRST, 3, march::F_NONE, false, true, true><<<blocks, 256, 0, st>>>(A, it); break;
         }
         return;
     }
     if (sc.ext) {  // non-solid textures or a Torus: the generic extended build
-        wf_bounce<NW, FIRST, 2, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<FIRST, 2, march::F_ANY, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (fkind != march::F_HEART) {  // another ray-marched function: the generic build
-        wf_bounce<NW, FIRST, 2, march::F_ANY><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<FIRST, 2, march::F_ANY><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     if (PT_WAVE_DIAG && diag) {  // (diagnostics builds)
-        wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it, diag);
-        return;
-    }
-    if (NW > 4) {  // deep stacks: the 2-wave budget (no spills)
-        wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it, diag);
         return;
     }
     if (sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0) {  // a large BVH and no marched shape (C5): the FMA slab
         switch (waves) {                                   // build without march pre-check or Heart code
-        case 4: wf_bounce<NW, FIRST, 4, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
-        case 5: wf_bounce<NW, FIRST, 5, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
-        default: wf_bounce<NW, FIRST, 3, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 4: wf_bounce<FIRST, 4, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        case 5: wf_bounce<FIRST, 5, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
+        default: wf_bounce<FIRST, 3, march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it); break;
         }
         return;
     }
     if (waves == 3 && sc.nnodes >= BIG_BVH_NODES) {  // the default budget, a large BVH with a marched shape
-        wf_bounce<NW, FIRST, 3, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
+        wf_bounce<FIRST, 3, march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it);
         return;
     }
     switch (waves) {  // Tuning::wf_bounce_waves
-    case 2: wf_bounce<NW, FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 4: wf_bounce<NW, FIRST, 4, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 5: wf_bounce<NW, FIRST, 5, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 6: wf_bounce<NW, FIRST, 6, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    case 8: wf_bounce<NW, FIRST, 8, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
-    default: wf_bounce<NW, FIRST, 3, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 2: wf_bounce<FIRST, 2, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 4: wf_bounce<FIRST, 4, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 5: wf_bounce<FIRST, 5, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 6: wf_bounce<FIRST, 6, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    case 8: wf_bounce<FIRST, 8, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
+    default: wf_bounce<FIRST, 3, march::F_HEART><<<blocks, 256, 0, st>>>(A, it); break;
     }
-}
-
-// The tail kernel's build for the scene (the bounce kernel's choice of march code and BVH walk).
-static void launch_tail(uint32_t blocks, hipStream_t st, const dev::Scene &sc, const WfArgs *A, int it, int fkind,
-                        uint32_t max_paths) {
-    if (sc.ext)
-        wf_tail<march::F_ANY, true, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
-    else if (fkind != march::F_HEART)
-        wf_tail<march::F_ANY, false, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
-    else if (sc.nnodes >= BIG_BVH_NODES && sc.nmarch == 0)
-        wf_tail<march::F_NONE, false, true><<<blocks, 256, 0, st>>>(A, it, max_paths);
-    else if (sc.nnodes >= BIG_BVH_NODES)
-        wf_tail<march::F_HEART, false, true><<<blocks, 256, 0, st>>>(A, it, max_paths);
-    else
-        wf_tail<march::F_HEART, false, false><<<blocks, 256, 0, st>>>(A, it, max_paths);
 }
 
 // Exactly the resident blocks of one kernel build (persistent grids).
@@ -1457,7 +1252,7 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    if (ws->device != dev || ws->side_priority != ws->tune.wf_side_priority) {  // streams and events belong to one device
+    if (ws->device != dev) {  // streams and events belong to one device
         // the previous frame must be done with the streams and the workspace
         if (ws->used && ws->done && (e = hipEventSynchronize(ws->done)) != hipSuccess) return e;
         free_args(ws);  // (the device blocks live on the old device)
@@ -1472,26 +1267,16 @@ static hipError_t ensure_streams(WaveWorkspace *ws, int slots) {
         if (ws->fork) (void)hipEventDestroy(ws->fork);
         if (ws->reduced) (void)hipEventDestroy(ws->reduced);
         if (ws->done) (void)hipEventDestroy(ws->done);
-        if (ws->bev) (void)hipEventDestroy(ws->bev);
-        if (ws->mev) (void)hipEventDestroy(ws->mev);
-        ws->fork = ws->reduced = ws->done = ws->bev = ws->mev = nullptr;
+        ws->fork = ws->reduced = ws->done = nullptr;
         ws->used = false;
         ws->device = dev;
-        ws->side_priority = ws->tune.wf_side_priority;
     }
     if (!ws->fork && (e = hipEventCreateWithFlags(&ws->fork, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->done && (e = hipEventCreateWithFlags(&ws->done, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->reduced && (e = hipEventCreateWithFlags(&ws->reduced, hipEventDisableTiming)) != hipSuccess) return e;
-    if (!ws->bev && (e = hipEventCreateWithFlags(&ws->bev, hipEventDisableTiming)) != hipSuccess) return e;
-    if (!ws->mev && (e = hipEventCreateWithFlags(&ws->mev, hipEventDisableTiming)) != hipSuccess) return e;
     if (!ws->args_ev && (e = hipEventCreateWithFlags(&ws->args_ev, hipEventDisableTiming)) != hipSuccess) return e;
     for (int k = 0; k < slots - 1; k++) {
-        if (!ws->side[k]) {
-            int lo = 0, hi = 0;  // least and greatest priority (greatest is numerically lowest)
-            if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return e;
-            const int pr = ws->tune.wf_side_priority < 0 ? lo : (ws->tune.wf_side_priority > 0 ? hi : 0);
-            if ((e = hipStreamCreateWithPriority(&ws->side[k], hipStreamNonBlocking, pr)) != hipSuccess) return e;
-        }
+        if (!ws->side[k] && (e = hipStreamCreateWithFlags(&ws->side[k], hipStreamNonBlocking)) != hipSuccess) return e;
         if (!ws->join[k] && (e = hipEventCreateWithFlags(&ws->join[k], hipEventDisableTiming)) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1506,8 +1291,7 @@ struct Slot {
     PathSoA set[2];  // iteration it reads set[it & 1] and writes set[(it + 1) & 1]
 };
 
-template <int NW>
-static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
+static hipError_t render_wave(const dev::Scene &sc, const FrameParams &P0, double *out, hipStream_t st,
                                  WaveWorkspace *ws, int fkind) {
     const Tuning &tu = ws->tune;
     // the launch's samples: the frame's, or a resumable frame's window [s_begin, s_end) of them
@@ -1622,28 +1406,15 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     for (int k = 0; k < slots; k++) sl[k].v.acc = acc;
     if ((size_t)(p - (char *)ws->base) > ws->bytes) return hipErrorOutOfMemory;
 
-    // persistent march grid: exactly the resident blocks of the device (or
-    // Tuning::wf_march_blocks_per_cu per CU, if fewer)
-    static const uint32_t march_resident = resident_blocks(wf_march<march::F_HEART>);
-    uint32_t march_blocks = march_resident;
-    if (tu.wf_march_blocks_per_cu > 0) {
-        int dev = 0, cus = 256;
-        hipDeviceProp_t pr;
-        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) cus = pr.multiProcessorCount;
-        const uint32_t want = (uint32_t)(cus * tu.wf_march_blocks_per_cu);
-        if (want < march_blocks) march_blocks = want;
-    }
+    // persistent march grid: exactly the resident blocks of the device (a half-machine grid measured slower)
+    static const uint32_t march_blocks = resident_blocks(wf_march<march::F_HEART>);
     const uint32_t march_slice = (uint32_t)tu.wf_march_slice;
-    // the tail kernel's persistent grid: its resident blocks (a launch that finds too many live paths ends at once)
-    static const uint32_t tail_blocks = resident_blocks(wf_tail<march::F_HEART, false, false>);
-    const uint32_t tail_paths = (uint32_t)tu.wf_tail_paths;
     const bool split = walk_split(sc, tu);
     // Chunk j of step k runs on stream j (its path-state slot); a step's chunks
-    // are enqueued iteration by iteration across the step.  With wf_pingpong the
-    // bounce launches form one chain across the streams (each waits for the
-    // previous one, in enqueue order), so one chunk's bounce (memory-bound)
-    // runs beside the other chunk's compaction and march (VALU-bound) instead
-    // of both chunks bouncing, then both marching, at the same time.
+    // are enqueued iteration by iteration across the step.  (Measured slower and
+    // removed in round 6, DESIGN.md §5: bounce or march launches chained across
+    // the streams, side streams at another priority, streams staggered by part
+    // of a chunk, a tail kernel running a chunk's last paths to their ends.)
     struct Chunk {
         uint32_t g0, gt, s0, ns;
         int slot;
@@ -1656,53 +1427,18 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
     uint32_t nchunks = (nsw + ns - 1) / ns;
     if (slots > 1 && nchunks > 1 && nchunks % (uint32_t)slots) nchunks += (uint32_t)slots - nchunks % (uint32_t)slots;
     if (nchunks > nsw) nchunks = nsw;
-    // Staggered streams (Tuning::wf_stagger): stream j > 0 starts with a chunk
-    // of j / slots of the samples and ends with one of (slots - j) / slots, so
-    // the streams run a chunk apart by 1 / slots of its length.  A chunk's last
-    // iterations are a few short, latency-bound launches (its march launches
-    // last as long as their slowest job whatever the queue length); streams in
-    // step reach those together and leave the device idle, staggered ones lay
-    // each tail beside another stream's full iterations.  The chunks of a
-    // group take consecutive sample ranges in the order they are expected to
-    // finish (which is the order of the per-pixel sums), so no reduce waits
-    // for a chunk that finishes later than its own.
-    const uint32_t S = (uint32_t)slots, R = nchunks / (S ? S : 1u);
-    const bool stagger = tu.wf_stagger && slots > 1 && nchunks % S == 0 && nsw / nchunks >= 2 * S;
+    const uint32_t S = (uint32_t)slots;
     std::vector<Chunk> chunk_list;
     uint32_t step0 = 0;
     for (uint32_t g0 = 0; g0 < ntiles; g0 += group_tiles) {
         const uint32_t gt = ntiles - g0 < group_tiles ? ntiles - g0 : group_tiles;
-        const size_t c0 = chunk_list.size();
-        std::vector<uint32_t> ticks;  // chunk sizes in 1/S of a chunk (stagger), or whole chunks
-        if (stagger) {
-            for (uint32_t k = 0; k <= R; k++) {
-                for (uint32_t j = 1; j < S; j++) {  // stream j: leading j/S, full chunks, trailing (S-j)/S
-                    chunk_list.push_back(Chunk{g0, gt, 0, 0, (int)j, step0 + k});
-                    ticks.push_back(k == 0 ? j : (k == R ? S - j : S));
-                }
-                if (k < R) {
-                    chunk_list.push_back(Chunk{g0, gt, 0, 0, 0, step0 + k});
-                    ticks.push_back(S);
-                }
-            }
-            step0 += R + 1;
-        } else {
-            for (uint32_t c = 0; c < nchunks; c++) {
-                chunk_list.push_back(Chunk{g0, gt, 0, 0, (int)(c % S), step0 + c / S});
-                ticks.push_back(1);
-            }
-            step0 += (nchunks + S - 1) / S;
-        }
-        uint64_t tot = 0, cum = 0;
-        for (uint32_t t : ticks) tot += t;
         uint32_t s0 = s_begin;
-        for (size_t c = 0; c < ticks.size(); c++) {
-            cum += ticks[c];
-            const uint32_t s1 = s_begin + (uint32_t)((uint64_t)nsw * cum / tot);  // <= ceil(nsw / nchunks) <= ns each
-            chunk_list[c0 + c].s0 = s0;
-            chunk_list[c0 + c].ns = s1 - s0;
+        for (uint32_t c = 0; c < nchunks; c++) {
+            const uint32_t s1 = s_begin + (uint32_t)((uint64_t)nsw * (c + 1) / nchunks);  // <= ceil(nsw / nchunks) <= ns
+            chunk_list.push_back(Chunk{g0, gt, s0, s1 - s0, (int)(c % S), step0 + c / S});
             s0 = s1;
         }
+        step0 += (nchunks + S - 1) / S;
     }
     // The launches' argument blocks (WfArgs): chunk ci at iteration parity h is block 2 ci + h.  They are
     // written to the pinned staging buffer, which the previous frame's copy must have read, and copied to the
@@ -1733,9 +1469,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
         for (int k = 0; k < slots - 1; k++)
             if ((e = hipStreamWaitEvent(ws->side[k], ws->fork, 0)) != hipSuccess) return e;
     }
-    // wf_pingpong bit 0: chain the bounce launches; bit 1: chain the march launches
-    const bool pingpong = (tu.wf_pingpong & 1) && slots > 1, mchain = (tu.wf_pingpong & 2) && slots > 1;
-    bool chained = false, mchained = false;  // ws->bev / ws->mev hold a launch to wait for
     for (size_t r0 = 0; r0 < chunk_list.size();) {
         size_t r1 = r0;  // the step's chunks [r0, r1), in sample order, at most one per stream
         while (r1 < chunk_list.size() && chunk_list[r1].step == chunk_list[r0].step) r1++;
@@ -1759,26 +1492,15 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 const uint32_t paths = ch.ns * ch.gt * TILE * TILE;
                 uint32_t bb = (paths + 255) / 256;
                 if (bb > WF_BOUNCE_CAP) bb = WF_BOUNCE_CAP;
-                if (tail_paths && it >= 1) {  // few live paths left: wf_tail runs them to their ends
-                    if ((e = timer_begin(ws->timer, cs, K_TAIL)) != hipSuccess) return e;
-                    launch_tail(tail_blocks, cs, sc, A, it, fkind, tail_paths);
-                    if ((e = hipGetLastError()) != hipSuccess) return e;
-                    if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
-                }
-                if (pingpong && chained && (e = hipStreamWaitEvent(cs, ws->bev, 0)) != hipSuccess) return e;
                 // iteration 0: slots [0, paths) are the chunk's camera rays
                 if ((e = timer_begin(ws->timer, cs, K_BOUNCE)) != hipSuccess) return e;
                 if (it == 0)
-                    launch_bounce<NW, true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves,
+                    launch_bounce<true>((paths + 255) / 256, cs, sc, A, 0, ws->diag, fkind, tu.wf_bounce_waves,
                                             split);
                 else
-                    launch_bounce<NW, false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves, split);
+                    launch_bounce<false>(bb, cs, sc, A, it, ws->diag, fkind, tu.wf_bounce_waves, split);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
-                if (pingpong) {
-                    if ((e = hipEventRecord(ws->bev, cs)) != hipSuccess) return e;
-                    chained = true;
-                }
                 if (it == iters - 1) continue;  // the last bounce only shades
                 // live list for it + 1 and march queue for it, both id-sorted
                 if ((e = timer_begin(ws->timer, cs, K_SELECT)) != hipSuccess) return e;
@@ -1796,7 +1518,7 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 if (split) {  // the new rays' BVH walk, over the live list of it + 1
                     if ((e = timer_begin(ws->timer, cs, K_WALK)) != hipSuccess) return e;
-                    if (!(PT_WALK_QN && sc.qnodes)) {  // (a tree without the quantized form)
+                    if (!sc.qnodes) {  // (a tree without the quantized form)
                         wf_walk<5, false><<<bb, 256, 0, cs>>>(A, it);
                     } else {
                         switch (tu.wf_walk) {  // the walk's register budget, waves per SIMD
@@ -1810,7 +1532,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                     if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
                 }
                 if (sc.nmarch == 0) continue;  // no ray-marched shape: the march queue is always empty
-                if (mchain && mchained && (e = hipStreamWaitEvent(cs, ws->mev, 0)) != hipSuccess) return e;
                 if ((e = timer_begin(ws->timer, cs, K_MARCH)) != hipSuccess) return e;
                 if (fkind != march::F_HEART)
                     wf_march<march::F_ANY><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
@@ -1820,10 +1541,6 @@ static hipError_t render_wave_nw(const dev::Scene &sc, const FrameParams &P0, do
                     wf_march<march::F_HEART><<<march_blocks, 256, 0, cs>>>(A, it, nullptr, march_slice);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
-                if (mchain) {
-                    if ((e = hipEventRecord(ws->mev, cs)) != hipSuccess) return e;
-                    mchained = true;
-                }
             }
         }
         // the per-pixel sums take the chunks in sample order (chunk_list order)
@@ -1887,9 +1604,8 @@ extern "C" int pt_march_regions(unsigned long long *out, int clear) {
 hipError_t launch_render_wave(const dev::Scene &sc, const FrameParams &P, double *out, hipStream_t st,
                               WaveWorkspace *ws, int fkind) {
     if (P.tile_count == 0 || P.spp == 0) return hipSuccess;
-    // the NW template only sizes the megakernel's register stacks; the
-    // wavefront keeps attenuation ids in HBM, so one build serves every depth
-    return render_wave_nw<4>(sc, P, out, st, ws, fkind);
+    // (the wavefront keeps attenuation ids in HBM, so one build serves every depth)
+    return render_wave(sc, P, out, st, ws, fkind);
 }
 
 }  // namespace pt

@@ -5,7 +5,7 @@ launches (before the bounce of their iteration) are summed per iteration, with t
 
     python scripts/kt_iters.py <kernel_trace.csv> [first_frame_index]
 
-A chunk starts with a first-iteration bounce (wf_bounce<.., true, ..>); iteration it of the chunk is its it-th
+A chunk starts with a first-iteration bounce (wf_bounce<true, ..>); iteration it of the chunk is its it-th
 bounce launch, and the march launch that follows it belongs to the same iteration.  Only frames before the
 count_work probe are counted.
 """
@@ -14,7 +14,7 @@ import csv
 import re
 import sys
 
-FIRST = re.compile(r"wf_bounce<\d+, true")  # a chunk's first-iteration bounce (the FIRST template argument)
+FIRST = re.compile(r"wf_bounce<true")  # a chunk's first-iteration bounce (the FIRST template argument)
 
 
 def main():

@@ -6,14 +6,14 @@ roofline.kernels[*].kernel_ms_avg (HIP events):
 
 <frames in the run> = warmup + steps + 1 (the roofline frame).  The roofline
 frame is the last frame before the count_work probe; a frame's chunks each
-start with one first-iteration bounce launch (wf_bounce<.., true, ..>).
+start with one first-iteration bounce launch (wf_bounce<true, ..>).
 """
 import collections
 import csv
 import re
 import sys
 
-FIRST = re.compile(r"wf_bounce<\d+, true")  # a chunk's first-iteration bounce (the FIRST template argument)
+FIRST = re.compile(r"wf_bounce<true")  # a chunk's first-iteration bounce (the FIRST template argument)
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 total_frames = int(sys.argv[2])

@@ -84,55 +84,3 @@ extern "C" long advance_check(long n, uint64_t seed) {
     return bad;
 }
 
-// grid_step / stays_in_binade (the drift-free sign proof, round 5): wherever stays_in_binade(v, up, |cp|, B)
-// holds for cp = grid_step(v, c), the B literal additions fl(v_j + c) are exactly v + j cp (compared for every j),
-// on n pseudo-random (v, c, B) with binade edges, round-half-even ties and both directions.  Returns
-// (mismatches) and sets *claimed to the number of cases where the claim was made (the test needs some).
-extern "C" long grid_step_check(long n, uint64_t seed, long *claimed) {
-    using namespace pt::march;
-    uint64_t s = seed;
-    auto next = [&s]() {
-        s += 0x9E3779B97F4A7C15ull;
-        uint64_t z = s;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-        return z ^ (z >> 31);
-    };
-    auto unit = [&]() { return (double)(next() >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0; };
-    long bad = 0, made = 0;
-    for (long i = 0; i < n; i++) {
-        const int mode = (int)(i % 5);
-        double v = unit() * ldexp(1.0, (int)(next() % 12) - 6);
-        double c = unit() * ldexp(1.0, -(int)(next() % 30) - 8);
-        const double B = (double)(1 + next() % 4000);
-        if (mode == 1) {  // starting next to a binade edge, moving toward it
-            const double e = ldexp(1.0, (int)(next() % 8) - 4);
-            v = e * (1.0 + ldexp((double)(next() % 64), -52));
-            c = -fabs(c);
-            if (next() & 1) v = -v, c = -c;
-        }
-        if (mode == 2) {  // just below the next edge, moving up
-            const double e = ldexp(1.0, (int)(next() % 8) - 4);
-            v = 2.0 * e * (1.0 - ldexp((double)(1 + next() % 4096), -53));
-            c = fabs(c);
-        }
-        if (mode == 3) {  // round-half-even ties: c an odd multiple of u / 2
-            const int e = ilogb(v);
-            c = ldexp(2.0 * (double)(next() % 1000) + 1.0, e - 53);
-        }
-        bool ok;
-        const double cp = grid_step(v, c, &ok);
-        if (!ok || !stays_in_binade(v, (v >= 0.0) == (c >= 0.0), fabs(cp), B)) continue;
-        made++;
-        double lit = v;
-        for (long j = 1; j <= (long)B; j++) {
-            lit = lit + c;
-            if (lit != v + (double)j * cp) {  // v + j cp is exact here: on v's grid, inside its binade
-                bad++;
-                break;
-            }
-        }
-    }
-    *claimed = made;
-    return bad;
-}

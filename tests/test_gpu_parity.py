@@ -221,29 +221,6 @@ def test_wavefront_chunk_size_invariance(pt, cornell):
     check_image(split, osc.render(96, 54, 4, 8, 31))
 
 
-def test_wavefront_tail_equals_iterations(pt, cornell):
-    """wf_tail (a chunk's last live paths run to their ends by one persistent launch) renders the bits of the
-    per-iteration launches: never (0), from the first bounce on (a 2^28 threshold), and part-way (300 paths, so
-    the switch falls in the middle of the chunks' iterations, a different one per chunk); depth 50 with the Heart,
-    two chunk streams, staggered and in step; and against the oracle."""
-    ps, osc = cornell
-    r = pt.HipRenderer(ps, depth=50)
-    cam, ip = ps.camera(), pt.ImageParams(64, 36)
-    r.set_option("engine", 2)  # wavefront
-    # 12 tiles x 4 spp per chunk: 2 chunks on 2 streams in step; staggered, stream 1 runs 2 + 2 spp
-    r.set_option("wf_paths", 256 * 12 * 4)
-    imgs = {}
-    for tail in (0, 1 << 28, 300):
-        for stagger in (0, 1):
-            r.set_option("wf_tail_paths", tail)
-            r.set_option("wf_stagger", stagger)
-            imgs[(tail, stagger)] = r.render(cam, ip, 8, seed=41)
-    base = imgs[(0, 0)]
-    for k, img in imgs.items():
-        assert np.array_equal(img, base), k
-    check_image(base, osc.render(64, 36, 8, 50, 41))
-
-
 def test_wavefront_chunks_and_tile_groups(pt, cornell):
     """A tiny path budget forces one-tile groups and one-sample chunks: the
     running per-pixel sums must still add samples in order."""

@@ -297,15 +297,17 @@ def test_tuning_options(pt, cornell):
     cam, ip = ps.camera(), pt.ImageParams(64, 40)
     base = r.render(cam, ip, 3, seed=4)
     for name, value in [("wf_slots", 1), ("wf_slots", 4), ("wf_march_slice", 0), ("wf_bounce_waves", 2),
-                        ("wf_march_blocks_per_cu", 1), ("wf_min_chunks", 3), ("engine", 1), ("mega_waves", 2),
-                        ("wf_side_priority", -1), ("wf_side_priority", 1), ("wf_pingpong", 1), ("bvh_leaf", 4),
-                        ("wf_stagger", 1), ("wf_tail_paths", 1 << 28), ("wf_walk", 0), ("wf_paths", 1 << 27)]:
+                        ("wf_min_chunks", 3), ("engine", 1), ("mega_waves", 2), ("bvh_leaf", 4), ("wf_walk", 0),
+                        ("wf_paths", 1 << 27)]:
         r.set_option(name, value)
         assert r.get_option(name) == value
         assert np.array_equal(r.render(cam, ip, 3, seed=4), base), (name, value)
         r.set_option(name, pt.OPTION_DEFAULTS[name])
     for bad in [("no_such_knob", 1), ("wf_slots", 0), ("wf_slots", 99), ("wf_bounce_waves", 7), ("bvh_leaf", 0),
-                ("bvh_leaf", 17), ("wf_walk", 7), ("wf_paths", 100), ("wf_stagger", 2)]:
+                ("bvh_leaf", 17), ("wf_walk", 7), ("wf_paths", 100),
+                # (removed in round 6: measured slower)
+                ("wf_stagger", 0), ("wf_tail_paths", 0), ("wf_pingpong", 0), ("wf_side_priority", 0),
+                ("wf_march_blocks_per_cu", 0)]:
         with pytest.raises(pt.PtError):
             r.set_option(*bad)
     r.start_rendering(cam, ip, 64, seed=4)

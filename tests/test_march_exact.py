@@ -124,12 +124,3 @@ def test_advance_equals_literal_adds(march_lib):
     assert march_lib.advance_check(20_000, 777) == 0
 
 
-def test_grid_step_claim_is_exact(march_lib):
-    """The sign proof's drift-free case (round 5): where stays_in_binade claims that a coordinate's B literal
-    steps stay in its binade, every one of them equals v + j * grid_step(v, c) exactly (200k random cases with
-    binade edges on both sides and round-half-even ties)."""
-    march_lib.grid_step_check.argtypes = [C.c_long, C.c_uint64, C.POINTER(C.c_long)]
-    march_lib.grid_step_check.restype = C.c_long
-    made = C.c_long()
-    assert march_lib.grid_step_check(200_000, 4242, C.byref(made)) == 0
-    assert made.value > 50_000, made.value

@@ -314,7 +314,7 @@ def test_bvh_fma_slab_tiny_direction_component(H):
 
 
 def test_large_tree_walk_far_origins_and_grazing_rays(H):
-    """The large-tree walk (fma = 1: FMA_SLAB, with PT_SLAB32 its f32 slab widened by the error bound; fma = 2:
+    """The large-tree walk (fma = 1: FMA_SLAB, its f32 slab widened by the error bound; fma = 2:
     the quantized nodes, their grid folded into the widened offsets) keeps
     every node that holds the closest hit: rays from origins up to 1e5 away, aimed to graze spheres' silhouettes
     (|t| large, planes far from the origin), and rays leaving from sphere surfaces at shallow angles."""

@@ -11,7 +11,7 @@ mkdir -p $OUT
 cd $R
 for rep in $(seq 1 $reps); do
     for v in "$@"; do
-        name=${v%%|*}; args=${v#*|}
+        name=${v%%|*}; args=${v#*|}; [ "$args" = "-" ] && args=""
         if [ "$name" = default ]; then lib=""; else lib=$R/variants/$name.so; fi
         echo "== $name rep $rep :: $args" >> $OUT/ab.log
         PT_AMD_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu-baseline --parity-pixels 64 --steps 3 $args \

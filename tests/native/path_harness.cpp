@@ -247,3 +247,25 @@ extern "C" int h_closest_nomarch(void *p, const double *ray, int fma, double *t)
     *t = best;
     return who;
 }
+
+// Per ray, the large-tree walk's node tests (the quantized binary layouts, wf_walk's build): counts[i] for ray i
+// (6 doubles each), with the closest hit's shape and t (the SIMT-cost analysis of scripts/walk_lanes.py).
+extern "C" int h_walk_counts(void *p, const double *rays, size_t n, uint32_t *counts, int *who, double *t) {
+    Bundle *b = (Bundle *)p;
+    if (!b->view.qnodes) return -1;
+    for (size_t i = 0; i < n; i++) {
+        dev::Ray r;
+        r.o = dev::v3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        r.d = dev::v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        const dev::V3 inv = dev::v3(1.0 / r.d.x, 1.0 / r.d.y, 1.0 / r.d.z);
+        Ctr c;
+        std::memset(&c, 0, sizeof c);
+        double best = __builtin_inf();
+        int w = -1;
+        dev::closest_nomarch<true, false, true, true>(b->view, r, inv, T_MIN, &best, &w, &c);
+        counts[i] = (uint32_t)c.c[C_NODE_SLABS];
+        who[i] = w;
+        t[i] = best;
+    }
+    return 0;
+}

@@ -35,12 +35,14 @@ def moved(scene, shift=(0.0, 0.0, 0.0), scale=1.0):
     return doc
 
 
-def render_both(pt, doc, w=128, h=72, spp=2, depth=8, seed=3):
+def render_both(pt, doc, w=128, h=72, spp=2, depth=8, seed=3, **opts):
     import torch
     text = json.dumps(doc)
     ps = pt.Scene.from_json(text, seed=1)
     r = pt.HipRenderer(ps, depth=depth)
     r.set_option("engine", 2)
+    for k, v in opts.items():
+        r.set_option(k, v)
     assert r.get_option("bvh_nodes") >= 1 << 15, "not the large-tree build"
     frame = torch.zeros(w * h * 3, dtype=torch.float64, device="cuda")
     r.render_device(ps.camera(), w, h, spp, seed, 0, 1, frame.data_ptr())
@@ -60,3 +62,14 @@ def test_large_tree_frames_far_and_scaled(pt, shift, scale):
     bad = np.flatnonzero(np.any(img != ref, axis=1))
     assert bad.size == 0, "%d of %d pixels differ (first %s)" % (bad.size, len(img), bad[:8].tolist())
     assert np.count_nonzero(ref) > 0
+
+
+@pytest.mark.parametrize("waves", [0, 4, 6, 8])
+def test_walk_register_budgets(pt, waves):
+    """Every register budget of the large-tree walk kernel (wf_walk 4, 6, 8 waves per SIMD, the 6- and 8-wave
+    builds with spills; 0: the walk inside the bounce kernel) renders the oracle's pixels (the default 5 is every
+    other test of this file)."""
+    import make_scenes
+    img, ref = render_both(pt, make_scenes.synthetic(40000), w=96, h=54, wf_walk=waves)
+    bad = np.flatnonzero(np.any(img != ref, axis=1))
+    assert len(bad) == 0, "%d of %d pixels differ" % (len(bad), len(img))

@@ -221,6 +221,14 @@ def test_wavefront_chunk_size_invariance(pt, cornell):
     check_image(split, osc.render(96, 54, 4, 8, 31))
 
 
+@pytest.mark.parametrize("waves", [2, 4, 5, 6, 8])
+def test_bounce_register_budgets(pt, cornell, waves):
+    """Every register budget of the bounce kernel (wf_bounce_waves; the 5-, 6- and 8-wave builds spill) renders
+    the oracle's pixels on the marched scene (the default 3 is every other test of this file)."""
+    img, ref = render_pair(pt, cornell, 64, 36, 3, 8, seed=21, wf_bounce_waves=waves, engine=2)
+    check_image(img, ref)
+
+
 def test_wavefront_chunks_and_tile_groups(pt, cornell):
     """A tiny path budget forces one-tile groups and one-sample chunks: the
     running per-pixel sums must still add samples in order."""

@@ -319,7 +319,7 @@ def parity_pixels(args):
     return np.unique(np.concatenate([grid, row, col])).astype(np.uint32)
 
 
-ROUNDS = ("r5", "r4", "r3", "r2", "r1")  # profiles/<round>/, newest first
+ROUNDS = ("r6", "r5", "r4", "r3", "r2", "r1")  # profiles/<round>/, newest first
 
 
 def parse_workload(w):

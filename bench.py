@@ -162,10 +162,10 @@ def launch_plan(args, env):
 def device_topology(infos, backend, comm_size):
     """What the ranks of a multi-rank bench ran on: each rank's LOCAL_RANK, device ordinal, PCI address and UUID
     (gathered to every rank), the backend and the communicator size, and the groups of ranks that shared one
-    physical device (by UUID, else PCI address)."""
-    by_dev = {}
+    physical device (the same PCI address and UUID)."""
+    by_dev = {}  # one physical device: the same PCI address and the same UUID (either alone could be blank)
     for i in infos:
-        by_dev.setdefault(i.get("uuid") or i.get("pci"), []).append(i["rank"])
+        by_dev.setdefault((i.get("pci"), i.get("uuid")), []).append(i["rank"])
     shared = sorted(sorted(v) for v in by_dev.values() if len(v) > 1)
     return {"backend": backend, "comm_size": comm_size, "ranks": sorted(infos, key=lambda i: i["rank"]),
             "distinct_devices": len(by_dev), "shared_devices": shared}

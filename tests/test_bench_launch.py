@@ -66,6 +66,9 @@ def test_topology_fields_and_refusal():
     rehearsal = bench.device_topology([dev(0, 0), dev(1, 0)], "gloo", 2)
     assert rehearsal["shared_devices"] == [[0, 1]] and bench.topology_refusal(rehearsal) is None
     assert "communicator size" in bench.topology_refusal(bench.device_topology([dev(0, 0)], "gloo", 2))
+    # a blank UUID (a driver that reports none) does not make distinct GPUs one device: the PCI address differs
+    blank = [dict(dev(r, r), uuid="") for r in range(8)]
+    assert bench.topology_refusal(bench.device_topology(blank, "nccl", 8)) is None
 
 
 def _gather_identities(rank, world, port, out):

@@ -352,3 +352,25 @@ def test_large_tree_walk_far_origins_and_grazing_rays(H):
         hits += w0 >= 0
     assert hits > 500
 
+
+
+def test_quantized_grid_refuses_unbounded_extents(H):
+    """Shapes near +-1e308 make the root box's extent overflow to inf: the quantized grid is not built (the walk
+    falls back to the 32-byte nodes) instead of the grid search looping forever, and hits still match."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "scenes"))
+    import make_scenes
+    H.h_closest_nomarch.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double)]
+    scene = make_scenes.synthetic(400)
+    far = json.loads(json.dumps(scene["shapes"][1]))
+    for j in range(40):  # (more than the wave-uniform list takes: the rest go to the BVH)
+        for sign in (1.0, -1.0):
+            s2 = json.loads(json.dumps(far))
+            s2["transform"]["translate"] = [sign * 1.5e308, 0.5 + j, 0.0]
+            scene["shapes"].append(s2)
+    pr = Pair(H, json.dumps(scene), seed=1)  # (returns: no endless loop in the grid builder)
+    t = C.c_double()
+    assert H.h_closest_nomarch(pr.h, (C.c_double * 6)(0, 2, 0, 0, -1, 0), 2, C.byref(t)) == -2  # no quantized nodes
+    for fma in (0, 1):
+        who = H.h_closest_nomarch(pr.h, (C.c_double * 6)(0, 2, 0, 0.01, -1, 0.02), fma, C.byref(t))
+        assert who >= 0

@@ -480,7 +480,6 @@ def main():
     k_end.clear()
     g_start.clear()
     g_end.clear()
-    pt.kernel_timing(r, True)  # per-kernel HIP events on the launch stream, timed steps only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -491,10 +490,17 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kt = pt.kernel_timing(r, False)
     guard_drops = pt.march_guard_drops(r)
     kernel_ms = sum(a.elapsed_time(b) for a, b in zip(k_start, k_end)) / max(1, len(k_start))
     gather_ms = sum(a.elapsed_time(b) for a, b in zip(g_start, g_end)) / max(1, len(g_start))
+    # parity is checked on the last timed frame (the one behind `value`): copy it out before the frames below
+    img = frame.view(-1, 3).cpu().numpy() if rank == 0 else None
+    # per-kernel launch durations: one more frame of the same workload with HIP events around every launch, after
+    # the timed region (the events' marker packets would add gaps between a small frame's ~50 dependent launches)
+    pt.kernel_timing(r, True)
+    step()
+    torch.cuda.synchronize()
+    kt = pt.kernel_timing(r, False)
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -502,8 +508,6 @@ def main():
     else:
         kernel_ms_max = kernel_ms
 
-    # parity is checked on the last timed frame (the one behind `value`): copy it out before the roofline leg
-    img = frame.view(-1, 3).cpu().numpy() if rank == 0 else None
     # roofline leg: one frame with every render kernel alone on the device (one chunk stream)
     kt_iso = None
     if not args.no_roofline_leg:
@@ -611,12 +615,12 @@ def main():
                          # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
                          # launches overlap the other stream's; these sums of launch durations can exceed the
                          # step time, and the whole path's rate is the frame's FLOPs over the frame time
-                         "timed_kernel_ms_per_step_summed_over_streams": {k: round(v[0] / args.steps, 3)
-                                                                          for k, v in kt.items()},
-                         "timed_kernel_ms_note": ("launch durations summed per kernel kind over %d concurrent "
-                                                  "chunk streams: they overlap, so a sum may exceed ms_per_step; "
-                                                  "per-kernel times of launches that run alone are in `kernels`"
-                                                  % slots),
+                         "kernel_ms_per_step_summed_over_streams": {k: round(v[0], 3) for k, v in kt.items()},
+                         "kernel_ms_note": ("one frame of the timed workload after the timed steps, HIP events "
+                                            "around each launch; launch durations summed per kernel kind over %d "
+                                            "concurrent chunk streams: they overlap, so a sum may exceed "
+                                            "ms_per_step; per-kernel times of launches that run alone are in "
+                                            "`kernels`" % slots),
                          "frame_kernels_ms": round(kernel_ms, 3), "frame_kernels_ms_max_rank": round(kernel_ms_max, 3),
                          "path_achieved": round(F * value * 1e6 / 1e12, 4),
                          "path_frac": round(F * value * 1e6 / 1e12 / FP64_PEAK_TFLOPS, 5)},
@@ -624,7 +628,7 @@ def main():
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
             "march_guard_drops": guard_drops,
-            "frame_plan": {"chunks_per_frame": kt["reduce"][1] // max(1, args.steps), "chunk_streams": slots,
+            "frame_plan": {"chunks_per_frame": kt["reduce"][1], "chunk_streams": slots,
                            "note": "the timed frames' sample chunks (one wf_reduce each) on this rank / first device"},
         }
         per_rank_tiles = [pt.shard_tiles(W, H, k, n_gpus) for k in range(n_gpus)]

@@ -23,6 +23,8 @@
 //   wf_reduce      per pixel, adds the chunk's sample radiances in sample
 //                  order to the running sum (the reference's in-order sum),
 //                  and divides by spp after the last chunk.
+//   wf_unwind      (chunks of few pixels) each slot's radiance, unwound in
+//                  place before wf_reduce, one thread per slot.
 //
 // Path state lives in HBM, structure-of-arrays, dense by position: bounce
 // `it` reads its k-th input from one state set at the position the live list
@@ -1002,7 +1004,31 @@ __global__ __launch_bounds__(256, WAVES) void wf_walk(const WfArgs *__restrict__
 // (dev::unwind; end_path left the leaf and the stack depth).  Sample by
 // sample: a version unwinding 8 samples level by level together needs more
 // registers and measured slower (the kernel is latency-bound: occupancy wins).
+constexpr uint32_t UNWIND_PIXELS = 1u << 18;  // chunks of fewer pixels unwind in their own pass (wf_unwind)
+// The unwind of every slot of the chunk, one thread per slot, in place (the leaf record's radiance becomes the
+// sample's): a thread per pixel unwinding its samples one after another waits for two dependent loads per sample.
 template <bool EXT>
+__global__ __launch_bounds__(256) void wf_unwind(const WfArgs *__restrict__ A) {
+    const WfArgs &args = kargs(A);
+    const WfView &v = args.v;
+    if (v.cnt[3]) return;  // a stopped frame's chunk
+    const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= v.ns * v.npix) return;
+    const uint32_t pl = id % v.npix;
+    uint32_t x, y, sl, pl2;
+    slot_pixel(args.P, v, pl, &x, &y, &sl, &pl2);
+    if (x >= args.P.width || y >= args.P.height) return;
+    double *rec = v.leaf + (size_t)id * 4;
+    const uint32_t fin = (uint32_t)__builtin_bit_cast(uint64_t, rec[3]);
+    if (fin == 0) return;
+    MemStack stk{v.ids + id, (size_t)v.cap, (int)fin, EXT ? v.att + id : nullptr};
+    const V3 c = unwind_mem<EXT>(args.sc, stk, dev::v3(rec[0], rec[1], rec[2]));
+    rec[0] = c.x;
+    rec[1] = c.y;
+    rec[2] = c.z;
+}
+
+template <bool EXT, bool UNWOUND = false>
 __global__ __launch_bounds__(256) void wf_reduce(const WfArgs *__restrict__ A, int first, int last,
                                                  double *__restrict__ out) {
     const WfArgs &args = kargs(A);
@@ -1029,6 +1055,13 @@ __global__ __launch_bounds__(256) void wf_reduce(const WfArgs *__restrict__ A, i
     V3 a = first == 1   ? dev::v3(0.0, 0.0, 0.0)
            : first == 2 ? dev::v3(dst[0], dst[1], dst[2])
                         : dev::v3(v.acc[pl * 3 + 0], v.acc[pl * 3 + 1], v.acc[pl * 3 + 2]);
+    if (UNWOUND) {
+#pragma unroll 4
+        for (uint32_t s = 0; s < v.ns; s++) {
+            const double *rec = v.leaf + ((size_t)s * v.npix + pl) * 4;
+            a = dev::add(a, dev::v3(rec[0], rec[1], rec[2]));
+        }
+    } else
     for (uint32_t s = 0; s < v.ns; s++) {
         const size_t id = (size_t)s * v.npix + pl;
         const double *rec = v.leaf + id * 4;
@@ -1552,13 +1585,31 @@ static hipError_t render_wave(const dev::Scene &sc, const FrameParams &P0, doubl
             const uint32_t npix = ch.gt * TILE * TILE;
             if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
             if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
+            // a chunk of few pixels unwinds its slots first, one thread each (a thread per pixel would be one wave
+            // per SIMD walking its samples' dependent loads one after another); larger chunks fill the machine
+            // with pixels, and the extra pass over the slots costs more than it saves (C1 +1.5 %, C2 -2.2 %,
+            // profiles/r6/ab/r6m_reduce_split_summary.txt)
+            const bool unwound = npix < UNWIND_PIXELS;
+            if (unwound) {
+                const uint32_t slots_c = ch.ns * npix;
+                if (sc.ext)
+                    wf_unwind<true><<<(slots_c + 255) / 256, 256, 0, cs>>>(A);
+                else
+                    wf_unwind<false><<<(slots_c + 255) / 256, 256, 0, cs>>>(A);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
             // first: 1 = sums from zero, 2 = from out's running sums; last: 1 = means, 2 = running sums to out
             const int first = ch.s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
             const int last = ch.s0 + ch.ns >= s_end ? (s_end == P0.spp ? 1 : 2) : 0;
-            if (sc.ext)
-                wf_reduce<true><<<(npix + 255) / 256, 256, 0, cs>>>(A, first, last, out);
+            const uint32_t rb = (npix + 255) / 256;
+            if (sc.ext && unwound)
+                wf_reduce<true, true><<<rb, 256, 0, cs>>>(A, first, last, out);
+            else if (sc.ext)
+                wf_reduce<true, false><<<rb, 256, 0, cs>>>(A, first, last, out);
+            else if (unwound)
+                wf_reduce<false, true><<<rb, 256, 0, cs>>>(A, first, last, out);
             else
-                wf_reduce<false><<<(npix + 255) / 256, 256, 0, cs>>>(A, first, last, out);
+                wf_reduce<false, false><<<rb, 256, 0, cs>>>(A, first, last, out);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             if (slots > 1 && (e = hipEventRecord(ws->reduced, cs)) != hipSuccess) return e;

@@ -336,8 +336,8 @@ int pt_render_stop_stats(pt_renderer *r, uint64_t *skipped, uint64_t *worked);
 /* Per-kernel launch timing of the render path (bench / roofline): returns
  * the summed HIP-event durations (ms) and launch counts per kernel kind since
  * the last call — [0] bounce, [1] march, [2] list compaction, [3] sample
- * reduce, [4] megakernel, [5] unused (always 0; was the wavefront tail kernel,
- * removed), [6] BVH walk (wf_walk) — into ms[nkinds] / launches[nkinds] (either may be
+ * reduce, [4] megakernel, [5] per-slot unwind before the reduce (wf_unwind;
+ * until round 6 the removed wavefront tail kernel), [6] BVH walk (wf_walk) — into ms[nkinds] / launches[nkinds] (either may be
  * NULL), then turns recording on (enable = 1) or off.  Events are recorded on
  * the stream each kernel is launched on.  PT_ERR_STATE while a render_start
  * frame is in flight (its band feeder records into the same timer). */

@@ -499,7 +499,7 @@ def march_jobs(renderer: "HipRenderer", jobs, status=False):
 
 
 # (slot 5 was the wavefront tail kernel, removed in round 6: always 0, not reported)
-KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", None, "walk"]
+KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", "unwind", "walk"]
 
 
 def kernel_timing(renderer: "HipRenderer", enable: bool = True) -> dict:

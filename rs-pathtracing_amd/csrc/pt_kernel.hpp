@@ -30,9 +30,8 @@ struct DeviceScene {
 // reused by every frame of a renderer.
 // Per-kernel launch timing (pt_kernel_timing): HIP events recorded on the
 // launch stream around every render-path kernel while enabled.
-// (kind 5 was the wavefront tail kernel, removed in round 6: its slot stays, always 0, so the ABI's array keeps
-// its layout)
-enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_RETIRED5 = 5, K_WALK = 6, K_KINDS = 7 };
+// (kind 5 was the wavefront tail kernel until round 6; it now times the per-slot unwind, wf_unwind)
+enum KernelKind : int { K_BOUNCE = 0, K_MARCH = 1, K_SELECT = 2, K_REDUCE = 3, K_MEGA = 4, K_UNWIND = 5, K_WALK = 6, K_KINDS = 7 };
 struct KernelTimer;
 KernelTimer *timer_new();
 void timer_free(KernelTimer *t);

@@ -1583,21 +1583,24 @@ static hipError_t render_wave(const dev::Scene &sc, const FrameParams &P0, doubl
             const hipStream_t cs = j == 0 ? st : ws->side[j - 1];
             const WfArgs *A = ad + 2 * c;
             const uint32_t npix = ch.gt * TILE * TILE;
-            if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
-            if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
             // a chunk of few pixels unwinds its slots first, one thread each (a thread per pixel would be one wave
-            // per SIMD walking its samples' dependent loads one after another); larger chunks fill the machine
-            // with pixels, and the extra pass over the slots costs more than it saves (C1 +1.5 %, C2 -2.2 %,
-            // profiles/r6/ab/r6m_reduce_split_summary.txt)
+            // per SIMD walking its samples' dependent loads one after another), before it waits for the previous
+            // chunk's sums.  Larger chunks fill the machine with pixels, and the extra pass over the slots costs
+            // more than it saves: C1 +1.5 %, but C2 -2.2 to -3.5 %, C5 -2.7 %, even C2 depth 50 -1.4 %
+            // (profiles/r6/ab/r6m_reduce_split_summary.txt, r6q_unwind_all_summary.txt)
             const bool unwound = npix < UNWIND_PIXELS;
             if (unwound) {
                 const uint32_t slots_c = ch.ns * npix;
+                if ((e = timer_begin(ws->timer, cs, K_UNWIND)) != hipSuccess) return e;
                 if (sc.ext)
                     wf_unwind<true><<<(slots_c + 255) / 256, 256, 0, cs>>>(A);
                 else
                     wf_unwind<false><<<(slots_c + 255) / 256, 256, 0, cs>>>(A);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
+                if ((e = timer_end(ws->timer, cs)) != hipSuccess) return e;
             }
+            if (slots > 1 && c > 0 && (e = hipStreamWaitEvent(cs, ws->reduced, 0)) != hipSuccess) return e;
+            if ((e = timer_begin(ws->timer, cs, K_REDUCE)) != hipSuccess) return e;
             // first: 1 = sums from zero, 2 = from out's running sums; last: 1 = means, 2 = running sums to out
             const int first = ch.s0 == s_begin ? (s_begin == 0 ? 1 : 2) : 0;
             const int last = ch.s0 + ch.ns >= s_end ? (s_end == P0.spp ? 1 : 2) : 0;

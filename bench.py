@@ -140,6 +140,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-roofline-leg", action="store_true", help="skip the one-stream roofline frame")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the frame with per-kernel HIP events after the timed steps (profiler runs)")
     ap.add_argument("--parity-pixels", type=int, default=0,
                     help="0: the stratified set (>= 8192 pixels); n: n random pixels")
     a = ap.parse_args()
@@ -497,10 +499,12 @@ def main():
     img = frame.view(-1, 3).cpu().numpy() if rank == 0 else None
     # per-kernel launch durations: one more frame of the same workload with HIP events around every launch, after
     # the timed region (the events' marker packets would add gaps between a small frame's ~50 dependent launches)
-    pt.kernel_timing(r, True)
-    step()
-    torch.cuda.synchronize()
-    kt = pt.kernel_timing(r, False)
+    kt = {}
+    if not args.no_kernel_timing:
+        pt.kernel_timing(r, True)
+        step()
+        torch.cuda.synchronize()
+        kt = pt.kernel_timing(r, False)
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if gloo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -532,8 +536,10 @@ def main():
         if multi:  # kernel timing covers the first device: its tile share
             share = pt.shard_tiles(W, H, 0, args.gpus) / pt.shard_tiles(W, H, 0, 1)
         samples_share = samples_frame * share
-        src = kt_iso if kt_iso is not None else kt
-        nfr = 1 if kt_iso is not None else args.steps
+        src = kt_iso if kt_iso is not None else kt  # each one frame
+        if not src:  # neither timing frame ran (--no-roofline-leg --no-kernel-timing: profiler passes)
+            src = {"bounce": (float("nan"), 1)}
+        nfr = 1
         walked = node_kernel(src) == "walk"  # the trace runs in wf_walk (large tree, no marched shape)
         bounce_ev = [k for k in FLOP_WEIGHTS if k not in MARCH_EVENTS and not (walked and k in WALK_EVENTS)]
         f_weights = {"march": flops_per_sample(counts, MARCH_EVENTS),
@@ -615,7 +621,7 @@ def main():
                          # the timed steps: two chunk streams run concurrently (pt_wave.hip), so one kernel's
                          # launches overlap the other stream's; these sums of launch durations can exceed the
                          # step time, and the whole path's rate is the frame's FLOPs over the frame time
-                         "kernel_ms_per_step_summed_over_streams": {k: round(v[0], 3) for k, v in kt.items()},
+                         "kernel_ms_per_step_summed_over_streams": {k: round(v[0], 3) for k, v in kt.items()} or None,
                          "kernel_ms_note": ("one frame of the timed workload after the timed steps, HIP events "
                                             "around each launch; launch durations summed per kernel kind over %d "
                                             "concurrent chunk streams: they overlap, so a sum may exceed "
@@ -628,7 +634,7 @@ def main():
                              "unit": "GB/s", "frac": out_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                              "bytes_per_launch": out_bytes, "note": "algorithmic: 24 B/pixel frame write"},
             "march_guard_drops": guard_drops,
-            "frame_plan": {"chunks_per_frame": kt["reduce"][1], "chunk_streams": slots,
+            "frame_plan": {"chunks_per_frame": kt["reduce"][1] if kt else None, "chunk_streams": slots,
                            "note": "the timed frames' sample chunks (one wf_reduce each) on this rank / first device"},
         }
         per_rank_tiles = [pt.shard_tiles(W, H, k, n_gpus) for k in range(n_gpus)]

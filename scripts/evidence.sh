@@ -22,7 +22,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 OUT=$R/gpurun_out/$tag
 mkdir -p $OUT
-ONE="--steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-roofline-leg"
+ONE="--steps 1 --warmup 0 --no-cpu-baseline --no-parity --no-roofline-leg --no-kernel-timing"
 declare -A SAMPLES=([c2]=530841600 [c3]=8493465600 [c5]=530841600 [c2d50]=530841600)
 declare -A WL=([c2]="cornell_box.json 1920x1080 256spp depth 8" [c3]="cornell_box.json 3840x2160 1024spp depth 8"
                [c5]="synthetic_100000 1920x1080 256spp depth 8" [c2d50]="cornell_box.json 1920x1080 256spp depth 50")
@@ -81,6 +81,6 @@ if [ "$what" = ranksim ]; then
     echo "ranksim c4 done" >> $OUT/progress.txt
 fi
 if [ "$what" = kt ] || [ "$what" = all ]; then
-    PROF_TIMEOUT=400 bash scripts/gpu.sh kt $tag/kt_default --no-cpu-baseline --no-parity
+    PROF_TIMEOUT=400 bash scripts/gpu.sh kt $tag/kt_default --no-cpu-baseline --no-parity --no-kernel-timing
     echo "kt done" >> $OUT/progress.txt
 fi

@@ -69,8 +69,8 @@ evidence)
     bash scripts/gpu.sh tests $tag
     bash scripts/gpu.sh smoke $tag
     bash scripts/gpu.sh bench $tag
-    bash scripts/gpu.sh kt $tag/kt_default --no-cpu-baseline --no-parity
-    KT_FRAMES=4 bash scripts/gpu.sh kt $tag/kt_one_stream --slots 1 --no-cpu-baseline --no-parity --no-roofline-leg ;;
+    bash scripts/gpu.sh kt $tag/kt_default --no-cpu-baseline --no-parity --no-kernel-timing
+    KT_FRAMES=4 bash scripts/gpu.sh kt $tag/kt_one_stream --slots 1 --no-cpu-baseline --no-parity --no-roofline-leg --no-kernel-timing ;;
 *)
     echo "usage: scripts/gpu.sh tests|smoke|bench|kt|pmc|sq|evidence <tag> [args]"; exit 2 ;;
 esac

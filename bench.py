@@ -695,7 +695,7 @@ def main():
                                        time.perf_counter() - t) if not args.parity_pixels
                                     else "%d random pixels" % len(px))
             rec["parity_frame"] = ("the last timed step's frame (the one behind `value`: %d chunks on %d chunk "
-                                   "streams%s), copied out before the roofline leg"
+                                   "streams%s), copied out before the kernel-timing and roofline frames"
                                    % (rec["frame_plan"]["chunks_per_frame"], slots,
                                       ", gathered from %d ranks" % world if world > 1 else ""))
         if world == 1 and not args.no_cpu_baseline:

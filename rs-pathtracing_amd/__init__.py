@@ -498,7 +498,7 @@ def march_jobs(renderer: "HipRenderer", jobs, status=False):
     return (t, st, it) if status else (t, st == 1, it)
 
 
-# (slot 5 was the wavefront tail kernel, removed in round 6: always 0, not reported)
+# (slot 5 was the wavefront tail kernel until round 6; it now times the per-slot unwind, wf_unwind)
 KERNEL_KINDS = ["bounce", "march", "select", "reduce", "megakernel", "unwind", "walk"]
 
 

@@ -131,7 +131,7 @@ __attribute__((visibility("hidden"))) void pt_set_last_error(const char *msg) { 
 #define PT_SRC_SHA "unknown"
 #endif
 const char *pt_version(void) {
-    return "rs-pathtracing-amd 0.4.1 (gfx950, f64 megakernel + wavefront march engine; src " PT_SRC_SHA ")";
+    return "rs-pathtracing-amd 0.4.2 (gfx950, f64 megakernel + wavefront march engine; src " PT_SRC_SHA ")";
 }
 uint32_t pt_abi_version(void) { return PT_ABI_VERSION; }
 

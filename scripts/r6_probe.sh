@@ -2,8 +2,10 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-mkdir -p gpurun_out/$1
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/$1/pytest_gpu.log 2>&1
-tail -2 gpurun_out/$1/pytest_gpu.log
-timeout -k 10 300 python -u scripts/interactive_bench.py --out gpurun_out/$1/interactive.jsonl > gpurun_out/$1/interactive.log 2>&1
-cut -c1-330 gpurun_out/$1/interactive.jsonl
+T=gpurun_out/$1
+mkdir -p $T
+for o in "" "--option wf_slots=3" "--option wf_min_chunks=4" "--option wf_paths=16777216" "--option wf_slots=3 --option wf_min_chunks=6" "--option wf_paths=25165824"; do
+    echo "== $o" >> $T/rs.txt
+    timeout -k 10 300 python -u scripts/rank_sim.py --worlds 8 $o 2>&1 | grep '"world"' >> $T/rs.txt
+done
+cat $T/rs.txt | cut -c1-200

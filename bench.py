@@ -33,6 +33,7 @@ After the timed steps (not part of `value`):
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -221,6 +222,18 @@ def spawn_ranks(args, argv):
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "bench.py")] + list(argv)
     print("bench.py: launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
     return subprocess.run(cmd).returncode
+
+
+def finite_or_null(x):
+    """The record with every non-finite float as null (strict JSON; a profiler pass without timing frames has no
+    per-kernel times, so its roofline fields are NaN)."""
+    if isinstance(x, float):
+        return x if math.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: finite_or_null(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [finite_or_null(v) for v in x]
+    return x
 
 
 def metric_name(args):
@@ -700,7 +713,7 @@ def main():
                                       ", gathered from %d ranks" % world if world > 1 else ""))
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(text, args)
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(finite_or_null(rec)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -98,3 +98,12 @@ def test_topology_gathered_over_two_ranks():
     for p in ps:
         p.join(timeout=60)
     assert res == [(0, 2, 2, None), (1, 2, 2, None)]
+
+
+def test_bench_line_is_strict_json():
+    """A profiler pass's record (no timing frames: NaN roofline fields) prints as strict JSON, NaN as null."""
+    import json
+    rec = bench.finite_or_null({"roofline": {"achieved": float("nan"), "frac": float("inf")}, "value": 2042.8,
+                                "kernels": [1.5, float("-inf")]})
+    text = json.dumps(rec, allow_nan=False)
+    assert json.loads(text) == {"roofline": {"achieved": None, "frac": None}, "value": 2042.8, "kernels": [1.5, None]}

@@ -2,10 +2,5 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-T=gpurun_out/$1
-mkdir -p $T
-for o in "" "--option wf_slots=3" "--option wf_min_chunks=4" "--option wf_paths=16777216" "--option wf_slots=3 --option wf_min_chunks=6" "--option wf_paths=25165824"; do
-    echo "== $o" >> $T/rs.txt
-    timeout -k 10 300 python -u scripts/rank_sim.py --worlds 8 $o 2>&1 | grep '"world"' >> $T/rs.txt
-done
-cat $T/rs.txt | cut -c1-200
+mkdir -p gpurun_out/$1
+bash scripts/abx.sh $1 1 "default|--config c5" "default|--config c5 --option wf_paths=33554432" "default|--config c5 --option wf_paths=67108864" "default|--config c5 --option wf_paths=100663296" "default|--config c5 --option wf_bounce_waves=4" "default|--config c5 --option wf_bounce_waves=5"

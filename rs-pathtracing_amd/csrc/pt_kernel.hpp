@@ -47,7 +47,7 @@ struct Tuning {
     int mega_waves = 4;              // megakernel register budget, waves per SIMD (2..5)
     int diag = 0;                    // bit 0: skip ray-marched shapes (a timing ablation, not the reference)
     int wf_slots = 2;                // sample chunks in flight, one stream each (1..4)
-    int64_t wf_paths = 0;            // path slots per chunk (256 .. 2^28; 0: 48M up to depth 16, else 128M).  Deep
+    int64_t wf_paths = 0;            // path slots per chunk (256 .. 2^28; 0: 48M up to depth 16, else 256M).  Deep
                                      // frames spend a quarter of a chunk in its tail of latency-bound iterations:
                                      // C2 depth 50 48M 1156, 96M 1226, 128M 1230-1241, 160M 1235 M samples/s (~58 GB
                                      // per chunk stream at 128M); at depth 8 128M costs the bounce 3 % (C2 2010 vs

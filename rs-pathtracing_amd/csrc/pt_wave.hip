@@ -1384,7 +1384,9 @@ static hipError_t render_wave(const dev::Scene &sc, const FrameParams &P0, doubl
     // until the plan fits the device memory the workspace may take (what is free plus what it holds now, less
     // 2 GiB): a deep textured frame's per-slot attenuation values ((depth + 1) * 24 B per path) would otherwise
     // ask for more than the device has (1080p, 256 spp, depth 50 at 128M paths needed ~430 GB).
-    uint32_t cap_want = tu.wf_paths ? (uint32_t)tu.wf_paths : (P0.depth > 16 ? 1u << 27 : 3u << 24);
+    // (deep frames: 256M paths, two chunks of a 1080p x 256-spp frame in one step, ~120 GB per chunk stream at depth
+    // 50: one tail of late iterations instead of two, C2 depth 50 1237 -> 1251, profiles/r6/ab/r6aa_*; 128M until round 6)
+    uint32_t cap_want = tu.wf_paths ? (uint32_t)tu.wf_paths : (P0.depth > 16 ? 1u << 28 : 3u << 24);
     Plan pl = plan_for(cap_want);
     {
         size_t free_b = 0, total_b = 0;

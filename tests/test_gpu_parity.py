@@ -411,8 +411,9 @@ def test_textured_frames(pt, name, seed, depth, monkeypatch):
 
 def test_textured_deep_frame_fits_device_memory(pt, monkeypatch):
     """A textured scene at the reference GUI's depth 50, 1920x1080, 128 spp: each path slot carries
-    (depth + 1) * 24 B of textured attenuation values, so the by-depth 128M-path chunk would need ~430 GB for two
-    chunk streams; the engine sizes its chunks to the device memory instead and the frame renders.  A sample of
+    (depth + 1) * 24 B of textured attenuation values, so the by-depth chunk (256M paths since round 6; 128M before)
+    would need ~430 GB per chunk stream; the engine sizes its chunks to the device memory instead and the frame
+    renders.  A sample of
     pixels is checked against the oracle at the texture tolerance."""
     import torch
     from conftest import ROOT, host_threads, scene_text
